@@ -1,0 +1,187 @@
+#!/usr/bin/env python3
+"""Headline benchmark: V-cycle grid-point-updates/sec at N=16384 (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+A step = one V-cycle (mg_inner, multigrid.cpp:17-92) + the residual and norm
+mg_outer computes after it (multigrid.cpp:112-113), with a fixed cycle count
+(no tolerance stop).  Workload: the reference problem (Gaussian u0,
+rotating velocity, nu=-4e-4, dt=dx/10) at N=16384, L=9 levels (coarsest 64),
+3 pre/post RB-GS sweeps, fp64; inputs resident in HBM before the timed region.
+
+value = (N-1)^2 * steps * ranks / max-over-ranks seconds.
+roofline: the dominant kernel is the fused RB-GS sweep on the finest level;
+achieved = 40 B x (N+1)^2 algorithmic bytes per launch / its mean duration
+(HIP events on the context stream, inside the timed region).
+cpu_baseline: rank 0, N=1 only: the reference's own mg_inner (oracle/_ref,
+built from the unmodified sources with the reference Makefile flags), one
+V-cycle of the same workload, OpenMP tasks on the host cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s HBM3E
+GS_BYTES_PER_PT = 40.0  # read u, rhs, v1, v2; write u
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--N", type=int, default=16384)
+    ap.add_argument("--levels", type=int, default=9)
+    ap.add_argument("--nsmooth", type=int, default=3)
+    ap.add_argument("--smoother", type=int, default=0, help="0 fused one-pass, 1 two-colour")
+    ap.add_argument("--cpu-baseline", choices=["auto", "off", "reference", "port"],
+                    default="auto")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-profile", action="store_true",
+                    help="do not record per-kernel HIP events in the timed region")
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """Reference V-cycle on the host (bounded sample: one V-cycle)."""
+    from oracle import oracle as O
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    N, L, nu = args.N, args.levels, -4e-4
+    kind = args.cpu_baseline
+    if kind == "auto":
+        kind = "reference" if O.ref_available() else "port"
+    if kind == "reference":
+        secs, setup, res = O.ref_time_vcycles(N, L, nu, 1, threads)
+        build = "reference gs.cpp+multigrid.cpp, -O0 -fopenmp (reference Makefile flags), OMP tasks"
+    else:
+        O.set_threads(threads)
+        u0, v1, v2 = O.init_problem(N)
+        dt = 1.0 / N / 10
+        t = O.Tower(u0, v1, v2, N, L)
+        del u0, v1, v2
+        O.compute_rhs(t.ufine, N, t.level("v1", 0), t.level("v2", 0), dt, nu, 1.0 / N,
+                      rhs=t.rhsfine)
+        t0 = time.perf_counter()
+        t.mg_inner(dt, nu)
+        O.residual(t.ufine, t.rhsfine, N, t.level("v1", 0), t.level("v2", 0), dt, nu, 1.0 / N,
+                   res=t.tmp)
+        secs = time.perf_counter() - t0
+        build = "oracle/mg_oracle.c restatement, gcc -O2 -fopenmp, OMP parallel-for rows"
+    return {"value": (N - 1) ** 2 / secs, "unit": "grid-point-updates/s", "cores": threads,
+            "kind": kind, "seconds_per_vcycle": secs,
+            "sample": f"1 V-cycle (mg_inner + residual + norm) at N={N}, L={L}, nu_smooth=3, "
+                      f"{threads} host threads; {build}"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import hpcclassmultigridproject_amd as pkg
+    from hpcclassmultigridproject_amd import _lib
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            sys.exit("for --gpus > 1 launch with torch.distributed.run --nproc-per-node N")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    N, L = args.N, args.levels
+    nu = -4e-4
+    dt = 1.0 / N / 10
+    u0, v1, v2 = pkg.init_problem(N, nthreads=16)
+    mg = pkg.Multigrid(N, L, dt, nu, nsmooth=args.nsmooth, device=local,
+                       smoother=args.smoother)
+    mg.upload(u0, v1, v2)
+    del u0, v1, v2
+    mg.rhs()
+    for _ in range(args.warmup):
+        mg.run_cycles(1)
+    mg.synchronize()
+    mg.profile_reset()
+    if not args.no_profile:
+        mg.profile(True)
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = None
+    for _ in range(args.steps):
+        res = mg.run_cycles(1)
+    mg.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-kernel HIP-event timings from the timed region
+    kernels = {}
+    for kind, name in _lib.KERNEL_NAMES.items():
+        n, ms, b = mg.profile_get(kind, -1)
+        if n:
+            kernels[name] = {"launches": n, "ms": round(ms, 4),
+                             "algo_GBs": round(b / (ms * 1e-3) / 1e9, 1) if ms > 0 else None}
+    n0, ms0, b0 = mg.profile_get(_lib.K_GS, 0)
+    mg.profile(False)
+    mg.close()
+
+    roof = None
+    if n0:
+        per_launch_bytes = GS_BYTES_PER_PT * (N + 1) ** 2
+        avg_s = ms0 * 1e-3 / n0
+        achieved = per_launch_bytes / avg_s / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": "k_gs_sweep<256> (fused one-pass RB-GS), finest level",
+                "per_launch_bytes": per_launch_bytes, "avg_launch_ms": round(avg_s * 1e3, 4)}
+
+    value = (N - 1) ** 2 * args.steps * world / elapsed
+    out = {
+        "metric": "V-cycle grid-point-updates/sec at N=16384; achieved HBM GB/s vs peak",
+        "value": value, "unit": "grid-point-updates/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic: the reference problem (Gaussian u0, rotating velocity), "
+                "generated on the host with glibc libm",
+        "config": {"workload": f"N={N} fp64 V-cycle, L={L} (coarsest {N >> (L - 1)}), "
+                               f"nu_smooth={args.nsmooth}, + residual/norm per step",
+                   "N": N, "levels": L, "nsmooth": args.nsmooth,
+                   "parallelism": "replicas" if world > 1 else "single",
+                   "last_residual": res},
+        "roofline": roof,
+        "kernels": kernels,
+    }
+    if rank == 0 and world == 1 and args.cpu_baseline != "off":
+        try:
+            out["cpu_baseline"] = cpu_baseline(args)
+        except Exception as e:   # the baseline is reported, never fatal
+            out["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,113 @@
+"""ctypes binding of libmgx.so (include/mgx.h).
+
+The shared library is built in-tree (``make -C hpcclassmultigridproject_amd/csrc``
+or ``__graft_entry__.build()``).  There is no fallback: if the library is
+missing or fails to load, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmgx.so")
+HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "mgx.h")
+
+MGX_OK, MGX_E_ARG, MGX_E_HIP, MGX_E_RCCL, MGX_E_NOCONV = 0, 1, 2, 3, 4
+TOWER_REFERENCE, TOWER_CORRECT = 0, 1
+K_GS, K_RESTRICT, K_PROLONG, K_RESNORM, K_COARSE, K_RHS, K_HALO = range(7)
+KERNEL_NAMES = {K_GS: "gs_sweep", K_RESTRICT: "residual_restrict", K_PROLONG: "prolong_add",
+                K_RESNORM: "residual_norm", K_COARSE: "coarse_solve", K_RHS: "compute_rhs",
+                K_HALO: "halo_exchange"}
+
+
+class MGXError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"mgx error {code}: {msg}")
+        self.code = code
+
+
+class Options(C.Structure):
+    """mgx_options (include/mgx.h)."""
+    _fields_ = [("nsmooth", C.c_int), ("shape", C.c_int), ("tower_mode", C.c_int),
+                ("device", C.c_int), ("coarse_tol", C.c_double), ("coarse_maxit", C.c_int),
+                ("max_cycle", C.c_int), ("smoother", C.c_int)]
+
+
+_dp = C.POINTER(C.c_double)
+_vp = C.c_void_p
+_L, _I, _D = C.c_long, C.c_int, C.c_double
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "mgx_last_error": (C.c_char_p, []),
+    "mgx_version": (_I, []),
+    "mgx_gauss_seidel": (_I, [_vp, _vp, _L, _vp, _vp, _D, _D, _D]),
+    "mgx_residual": (_I, [_vp, _vp, _vp, _L, _vp, _vp, _D, _D, _D]),
+    "mgx_compute_norm": (_I, [_vp, _L, _dp]),
+    "mgx_prolongation": (_I, [_vp, _vp, _L]),
+    "mgx_restriction": (_I, [_vp, _vp, _L]),
+    "mgx_compute_rhs": (_I, [_vp, _vp, _L, _vp, _vp, _D, _D, _D]),
+    "mgx_init_problem": (_I, [_vp, _vp, _vp, _L, _I]),
+    "mgx_default_options": (None, [C.POINTER(Options)]),
+    "mgx_timestepper": (_I, [_vp, _vp, _vp, _vp, _D, _I, _L, _D, _D, _D, _D, _I]),
+    "mgx_timestepper_ex": (_I, [_vp, _vp, _vp, _vp, _D, _I, _L, _D, _D, _D, _D,
+                                C.POINTER(Options), C.POINTER(_I)]),
+    "mgx_create": (_I, [C.POINTER(_vp), _L, _I, _D, _D, C.POINTER(Options)]),
+    "mgx_destroy": (_I, [_vp]),
+    "mgx_upload": (_I, [_vp, _vp, _vp, _vp]),
+    "mgx_download": (_I, [_vp, _vp]),
+    "mgx_upload_device": (_I, [_vp, _vp, _vp, _vp]),
+    "mgx_download_device": (_I, [_vp, _vp]),
+    "mgx_rhs": (_I, [_vp]),
+    "mgx_gs": (_I, [_vp, _I, _I]),
+    "mgx_residual_norm": (_I, [_vp, _I, _dp]),
+    "mgx_restrict": (_I, [_vp, _I]),
+    "mgx_prolong_add": (_I, [_vp, _I]),
+    "mgx_vcycle": (_I, [_vp]),
+    "mgx_mg_outer": (_I, [_vp, _D, C.POINTER(_I), _dp, _dp]),
+    "mgx_step": (_I, [_vp, _D, C.POINTER(_I)]),
+    "mgx_run_cycles": (_I, [_vp, _I, _dp]),
+    "mgx_level_n": (_I, [_vp, _I, C.POINTER(_L)]),
+    "mgx_download_level": (_I, [_vp, _I, _I, _vp]),
+    "mgx_coarse_iterations": (_I, [_vp, C.POINTER(_L)]),
+    "mgx_stream": (_I, [_vp, C.POINTER(_vp)]),
+    "mgx_synchronize": (_I, [_vp]),
+    "mgx_profile_enable": (_I, [_vp, _I]),
+    "mgx_profile_reset": (_I, [_vp]),
+    "mgx_profile_get": (_I, [_vp, _I, _I, C.POINTER(_L), _dp, _dp]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libmgx.so (once).  Raises if it is missing: no fallback path."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MGXError(-1, f"{LIB_PATH} is not built: run __graft_entry__.build() "
+                               "or make -C hpcclassmultigridproject_amd/csrc")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int, allow=()):
+    if rc != MGX_OK and rc not in allow:
+        raise MGXError(rc, lib().mgx_last_error().decode())
+    return rc
+
+
+def default_options(**kw) -> Options:
+    o = Options()
+    lib().mgx_default_options(C.byref(o))
+    for k, v in kw.items():
+        if not hasattr(o, k):
+            raise TypeError(f"unknown option {k}")
+        setattr(o, k, v)
+    return o

@@ -1,0 +1,79 @@
+// kernels.h -- internal launch interface of the CDNA4 stencil kernels.
+//
+// Two layouts:
+//   * reference layout: row-major, row pitch n+1 (gs.cpp:44), used by the
+//     raw-pointer gs.h mirror ops (scalar, one point per lane);
+//   * tower layout: row pitch P = round_up(n+1, 16) doubles (rows 128-B
+//     aligned, pair (2c, 2c+1) 16-B aligned) used by the context path, one
+//     column pair per lane, 16-B loads/stores.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace mgx {
+
+// Per-level Crank-Nicolson operator constants, computed on the host with the
+// reference's own expressions: rr = 0.5*k/(h*h) (gs.cpp:9-11),
+// dgs = 1.0-4.0*rr*nu (gs.cpp:130, :75), drhs = 1.0+4.0*rr*nu (gs.cpp:44).
+struct Coef {
+    double rr, nu, h, dgs, drhs;
+};
+Coef make_coef(double k, double nu, double h);
+
+inline long tower_pitch(long n) { return (n + 1 + 15) / 16 * 16; }
+
+// ---------------------------------------------------------------- reference layout
+void launch_raw_gs_colour(double *u, const double *rhs, const double *v1, const double *v2,
+                          long n, Coef c, int colour, hipStream_t s);
+void launch_raw_residual(double *res, const double *u, const double *rhs, const double *v1,
+                         const double *v2, long n, Coef c, hipStream_t s);
+void launch_raw_rhs(double *rhs, const double *u, const double *v1, const double *v2, long n,
+                    Coef c, hipStream_t s);
+void launch_raw_prolongation(double *up, const double *u, long n, hipStream_t s);
+// injection: dst[I*(m)+J] = src[2I*src_pitch + 2J], 0<=I,J<m; pitches in doubles
+void launch_injection(double *dst, long dst_pitch, const double *src, long src_pitch, long m,
+                      hipStream_t s);
+
+// Sum of squares of the interior of an (n+1)^2 field with row pitch `pitch`,
+// deterministic two-stage reduction; result written to *out (device) as sqrt.
+// `partials` must hold norm_partials_size() doubles.
+int norm_partials_size();
+void launch_norm(const double *res, long n, long pitch, double *partials, double *out,
+                 hipStream_t s);
+
+// ---------------------------------------------------------------- tower layout
+// One full red-black sweep, out of place: uout = GS(uin).  Every point of
+// uout (boundary included) is written.  zero_in: uin is taken as all zeros.
+void launch_gs_sweep(const double *uin, double *uout, const double *rhs, const double *v1,
+                     const double *v2, long n, long pitch, Coef c, bool zero_in,
+                     hipStream_t s);
+// One colour, in place (two launches make a sweep).  Reference for A/B timing.
+void launch_gs_colour(double *u, const double *rhs, const double *v1, const double *v2,
+                      long n, long pitch, Coef c, int colour, hipStream_t s);
+// residual at the fine even-even interior points written straight into the
+// coarse rhs: rhsc[I][J] = res(2I, 2J), 1<=I,J<=n/2-1 (residual + restriction,
+// multigrid.cpp:73-75).  Coarse boundary untouched.
+void launch_residual_restrict(const double *u, const double *rhs, const double *v1,
+                              const double *v2, long n, long pitch, Coef c, double *rhsc,
+                              long pitchc, hipStream_t s);
+// residual + sum of squares (not stored): partial sums -> norm into *out.
+void launch_residual_norm(const double *u, const double *rhs, const double *v1,
+                          const double *v2, long n, long pitch, Coef c, double *partials,
+                          double *out, hipStream_t s);
+// residual stored (interior) into res (tower layout).
+void launch_residual(double *res, const double *u, const double *rhs, const double *v1,
+                     const double *v2, long n, long pitch, Coef c, hipStream_t s);
+// uf += P(uc), every fine point (multigrid.cpp:81-83), nc = coarse n.
+void launch_prolong_add(double *uf, long pitchf, const double *uc, long pitchc, long nc,
+                        hipStream_t s);
+void launch_rhs(double *rhs, const double *u, const double *v1, const double *v2, long n,
+                long pitch, Coef c, hipStream_t s);
+// Coarsest-level solve in one workgroup: repeat {GS; residual; norm} while
+// norm > tol and it < maxit (multigrid.cpp:58-65), in place on u.
+// zero_first: u = 0 before the first sweep.  stats[0] += iterations,
+// stats[1] = last norm.
+void launch_coarse_solve(double *u, const double *rhs, const double *v1, const double *v2,
+                         long n, long pitch, Coef c, double tol, int maxit, bool zero_first,
+                         double *stats, hipStream_t s);
+constexpr long kCoarseOneWgMaxN = 256;
+
+}  // namespace mgx

@@ -1,0 +1,710 @@
+// mgx.hip -- context, V-cycle orchestration and the C ABI of include/mgx.h.
+//
+// Host control flow mirrors the reference solver (multigrid.cpp:17-186) call
+// for call; every stencil op is a CDNA4 kernel from kernels.hip on the
+// context's stream.  The level towers live in HBM in the "tower layout"
+// (row pitch round_up(n+1,16) doubles); u has two buffers per level because
+// the one-pass smoother is out of place (ping-pong).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/mgx.h"
+#include "kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                     \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            return fail(MGX_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+#define CHK(expr)              \
+    do {                       \
+        int rc_ = (expr);      \
+        if (rc_) return rc_;   \
+    } while (0)
+
+struct Level {
+    long n = 0, pitch = 0;
+    double *u[2] = {nullptr, nullptr};
+    int cur = 0;
+    bool zero = false;   // u is logically all zeros (multigrid.cpp:77), not yet written
+    double *rhs = nullptr, *v1 = nullptr, *v2 = nullptr;
+    mgx::Coef coef{};
+    double M() const { return double(n + 1) * double(n + 1); }
+    double *U() const { return u[cur]; }
+};
+
+struct ProfRec {
+    int kind, level;
+    double bytes;
+    hipEvent_t e0, e1;
+};
+
+}  // namespace
+
+struct mgx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    long N = 0;
+    int L = 0;
+    double dt = 0, nu = 0;
+    mgx_options opt{};
+    std::vector<Level> lv;
+    double *partials = nullptr;   // norm partial sums
+    double *dscal = nullptr;      // [0] norm, [2..3] coarse stats (iterations, last norm)
+    double *hscal = nullptr;      // pinned host mirror
+    double *stage[2] = {nullptr, nullptr};   // reference-layout (N+1)^2 staging
+    // profiling
+    bool prof = false;
+    std::vector<ProfRec> pending;
+    std::vector<hipEvent_t> pool;
+    double sum_ms[MGX_K_COUNT][64] = {};
+    double sum_bytes[MGX_K_COUNT][64] = {};
+    long count[MGX_K_COUNT][64] = {};
+};
+
+namespace {
+
+int check_launch(const char *what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(MGX_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+    return MGX_OK;
+}
+
+hipEvent_t take_event(mgx_ctx *c) {
+    if (!c->pool.empty()) {
+        hipEvent_t e = c->pool.back();
+        c->pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+// Launch helper: records HIP events around the launch when profiling is on.
+template <class F>
+int launch(mgx_ctx *c, int kind, int level, double bytes, F &&f) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (c->prof) {
+        e0 = take_event(c);
+        e1 = take_event(c);
+        if (e0) (void)hipEventRecord(e0, c->stream);
+    }
+    f();
+    CHK(check_launch("kernel launch"));
+    if (c->prof && e0 && e1) {
+        (void)hipEventRecord(e1, c->stream);
+        c->pending.push_back({kind, level, bytes, e0, e1});
+    }
+    return MGX_OK;
+}
+
+int prof_flush(mgx_ctx *c) {
+    if (c->pending.empty()) return MGX_OK;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (auto &r : c->pending) {
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, r.e0, r.e1));
+        int lvl = r.level < 0 ? 0 : (r.level > 63 ? 63 : r.level);
+        c->sum_ms[r.kind][lvl] += ms;
+        c->sum_bytes[r.kind][lvl] += r.bytes;
+        c->count[r.kind][lvl] += 1;
+        c->pool.push_back(r.e0);
+        c->pool.push_back(r.e1);
+    }
+    c->pending.clear();
+    return MGX_OK;
+}
+
+// ---------------------------------------------------------------- level ops
+int materialize(mgx_ctx *c, int l) {
+    Level &L = c->lv[l];
+    if (!L.zero) return MGX_OK;
+    HIPCHK(hipMemsetAsync(L.U(), 0, sizeof(double) * L.pitch * (L.n + 1), c->stream));
+    L.zero = false;
+    return MGX_OK;
+}
+
+// `sweeps` RB-GS sweeps (gauss_seidel, gs.cpp:109).
+int op_gs(mgx_ctx *c, int l, int sweeps) {
+    Level &L = c->lv[l];
+    for (int k = 0; k < sweeps; ++k) {
+        if (c->opt.smoother == 0) {
+            const bool z = L.zero;
+            CHK(launch(c, MGX_K_GS, l, 40.0 * L.M(), [&] {
+                mgx::launch_gs_sweep(L.u[L.cur], L.u[L.cur ^ 1], L.rhs, L.v1, L.v2, L.n, L.pitch,
+                                     L.coef, z, c->stream);
+            }));
+            L.cur ^= 1;
+            L.zero = false;
+        } else {
+            CHK(materialize(c, l));
+            CHK(launch(c, MGX_K_GS, l, 40.0 * L.M(), [&] {
+                mgx::launch_gs_colour(L.U(), L.rhs, L.v1, L.v2, L.n, L.pitch, L.coef, 0,
+                                      c->stream);
+                mgx::launch_gs_colour(L.U(), L.rhs, L.v1, L.v2, L.n, L.pitch, L.coef, 1,
+                                      c->stream);
+            }));
+        }
+    }
+    return MGX_OK;
+}
+
+// residual + compute_norm on level l, norm read back to the host (the one
+// host sync per cycle, gs.cpp:86 / multigrid.cpp:105,113).
+int op_residual_norm(mgx_ctx *c, int l, double *norm, double bytes_per_pt = 48.0) {
+    CHK(materialize(c, l));
+    Level &L = c->lv[l];
+    CHK(launch(c, MGX_K_RESNORM, l, bytes_per_pt * L.M(), [&] {
+        mgx::launch_residual_norm(L.U(), L.rhs, L.v1, L.v2, L.n, L.pitch, L.coef, c->partials,
+                                  c->dscal, c->stream);
+    }));
+    HIPCHK(hipMemcpyAsync(c->hscal, c->dscal, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    *norm = c->hscal[0];
+    return MGX_OK;
+}
+
+// residual -> restriction into rhs[l+1]; u[l+1] = 0 (multigrid.cpp:73-77).
+int op_restrict(mgx_ctx *c, int l) {
+    CHK(materialize(c, l));
+    Level &F = c->lv[l], &C = c->lv[l + 1];
+    CHK(launch(c, MGX_K_RESTRICT, l, 40.0 * F.M() + 24.0 * C.M(), [&] {
+        mgx::launch_residual_restrict(F.U(), F.rhs, F.v1, F.v2, F.n, F.pitch, F.coef, C.rhs,
+                                      C.pitch, c->stream);
+    }));
+    C.zero = true;
+    return MGX_OK;
+}
+
+// u[l] += prolongation(u[l+1]) (multigrid.cpp:81-83).
+int op_prolong_add(mgx_ctx *c, int l) {
+    CHK(materialize(c, l));
+    CHK(materialize(c, l + 1));
+    Level &F = c->lv[l], &C = c->lv[l + 1];
+    CHK(launch(c, MGX_K_PROLONG, l, 32.0 * F.M() + 8.0 * C.M(), [&] {
+        mgx::launch_prolong_add(F.U(), F.pitch, C.U(), C.pitch, C.n, c->stream);
+    }));
+    return MGX_OK;
+}
+
+// Coarsest level: GS until |r| <= coarse_tol or coarse_maxit (multigrid.cpp:55-65).
+int op_coarse(mgx_ctx *c, int l) {
+    Level &L = c->lv[l];
+    if (L.n <= mgx::kCoarseOneWgMaxN) {
+        const bool z = L.zero;
+        CHK(launch(c, MGX_K_COARSE, l, 88.0 * L.M(), [&] {
+            mgx::launch_coarse_solve(L.U(), L.rhs, L.v1, L.v2, L.n, L.pitch, L.coef,
+                                     c->opt.coarse_tol, c->opt.coarse_maxit, z, c->dscal + 2,
+                                     c->stream);
+        }));
+        L.zero = false;
+        return MGX_OK;
+    }
+    int it = 0;
+    double res = 1.0;
+    while (it < c->opt.coarse_maxit && res > c->opt.coarse_tol) {
+        CHK(op_gs(c, l, 1));
+        CHK(op_residual_norm(c, l, &res, 48.0));
+        ++it;
+    }
+    c->hscal[4] += it;
+    return MGX_OK;
+}
+
+// mg_inner (multigrid.cpp:17-92).
+int op_vcycle(mgx_ctx *c, int l) {
+    for (int sh = 0; sh < c->opt.shape; ++sh) {
+        if (l == c->L - 1) {
+            CHK(op_coarse(c, l));
+        } else {
+            CHK(op_gs(c, l, c->opt.nsmooth));
+            CHK(op_restrict(c, l));
+            CHK(op_vcycle(c, l + 1));
+            CHK(op_prolong_add(c, l));
+            CHK(op_gs(c, l, c->opt.nsmooth));
+        }
+    }
+    return MGX_OK;
+}
+
+int op_rhs(mgx_ctx *c) {
+    CHK(materialize(c, 0));
+    Level &L = c->lv[0];
+    return launch(c, MGX_K_RHS, 0, 32.0 * L.M(), [&] {
+        mgx::launch_rhs(L.rhs, L.U(), L.v1, L.v2, L.n, L.pitch, L.coef, c->stream);
+    });
+}
+
+// mg_outer (multigrid.cpp:97-120).
+int op_mg_outer(mgx_ctx *c, double tol, int *cycles, double *res0_out, double *res_out) {
+    double res0 = 0, res = 0;
+    CHK(op_residual_norm(c, 0, &res0));
+    res = res0;
+    int iter = 0;
+    for (; iter < c->opt.max_cycle && res / res0 > tol; ++iter) {
+        CHK(op_vcycle(c, 0));
+        CHK(op_residual_norm(c, 0, &res));
+    }
+    if (cycles) *cycles = iter;
+    if (res0_out) *res0_out = res0;
+    if (res_out) *res_out = res;
+    if (iter == c->opt.max_cycle) return fail(MGX_E_NOCONV, "mg_outer did not converge");
+    return MGX_OK;
+}
+
+// Coarse velocity tower (multigrid.cpp:148-160).  Reference mode reproduces
+// the reference's index arithmetic on flat (n/2+1)^2 buffers, zero filled
+// (SURVEY K2); correct mode injects every level from the one above.
+int build_tower(mgx_ctx *c) {
+    const long N = c->N;
+    for (int f = 0; f < 2; ++f) {
+        double *fine = f == 0 ? c->lv[0].v1 : c->lv[0].v2;
+        if (c->opt.tower_mode == MGX_TOWER_CORRECT) {
+            for (int l = 1; l < c->L; ++l) {
+                Level &A = c->lv[l - 1], &B = c->lv[l];
+                const double *src = f == 0 ? A.v1 : A.v2;
+                double *dst = f == 0 ? B.v1 : B.v2;
+                mgx::launch_injection(dst, B.pitch, src, A.pitch, B.n + 1, c->stream);
+                CHK(check_launch("injection"));
+            }
+            continue;
+        }
+        if (c->L < 2) continue;
+        // flat level-0 copy of the fine field in the reference layout
+        HIPCHK(hipMemcpy2DAsync(c->stage[0], (N + 1) * sizeof(double), fine,
+                                c->lv[0].pitch * sizeof(double), (N + 1) * sizeof(double), N + 1,
+                                hipMemcpyDeviceToDevice, c->stream));
+        const long ni = (N >> 1) + 1;   // multigrid.cpp:150
+        for (int l = 1; l < c->L; ++l) {
+            double *prev = c->stage[(l - 1) & 1], *next = c->stage[l & 1];
+            HIPCHK(hipMemsetAsync(next, 0, sizeof(double) * ni * ni, c->stream));
+            // restriction(vtow[l], vtow[l-1], ni-1): next[I*(ni/2... )] per gs.cpp:283
+            const long nr = ni - 1;   // the "n" passed to restriction
+            mgx::launch_injection(next, nr / 2 + 1, prev, nr + 1, nr / 2 + 1, c->stream);
+            CHK(check_launch("tower injection"));
+            Level &B = c->lv[l];
+            double *dst = f == 0 ? B.v1 : B.v2;
+            // level l reads its buffer with its own width n_l+1 (multigrid.cpp:46-47)
+            HIPCHK(hipMemcpy2DAsync(dst, B.pitch * sizeof(double), next,
+                                    (B.n + 1) * sizeof(double), (B.n + 1) * sizeof(double),
+                                    B.n + 1, hipMemcpyDeviceToDevice, c->stream));
+        }
+    }
+    return MGX_OK;
+}
+
+void free_ctx(mgx_ctx *c) {
+    if (!c) return;
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto &L : c->lv) {
+        (void)hipFree(L.u[0]);
+        (void)hipFree(L.u[1]);
+        (void)hipFree(L.rhs);
+        (void)hipFree(L.v1);
+        (void)hipFree(L.v2);
+    }
+    (void)hipFree(c->partials);
+    (void)hipFree(c->dscal);
+    (void)hipFree(c->stage[0]);
+    (void)hipFree(c->stage[1]);
+    if (c->hscal) (void)hipHostFree(c->hscal);
+    for (auto &r : c->pending) {
+        (void)hipEventDestroy(r.e0);
+        (void)hipEventDestroy(r.e1);
+    }
+    for (auto e : c->pool) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+bool is_pow2(long n) { return n >= 2 && (n & (n - 1)) == 0; }
+
+// raw-op scratch (norm partials + result), shared by the gs.h-mirror entry points
+std::mutex g_raw_mu;
+double *g_raw_scratch = nullptr;
+int g_raw_dev = -1;
+
+int raw_scratch(double **p) {
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    if (!g_raw_scratch || g_raw_dev != dev) {
+        HIPCHK(hipMalloc(&g_raw_scratch, sizeof(double) * (mgx::norm_partials_size() + 8)));
+        g_raw_dev = dev;
+    }
+    *p = g_raw_scratch;
+    return MGX_OK;
+}
+
+}  // namespace
+
+// =================================================================== C ABI
+extern "C" {
+
+const char *mgx_last_error(void) { return g_err.c_str(); }
+int mgx_version(void) { return 100; }
+
+void mgx_default_options(mgx_options *o) {
+    o->nsmooth = 3;          // multigrid.cpp:41
+    o->shape = 1;            // multigrid.cpp:241
+    o->tower_mode = MGX_TOWER_REFERENCE;
+    o->device = -1;          // current device
+    o->coarse_tol = 1e-5;    // multigrid.cpp:60
+    o->coarse_maxit = 1000;  // multigrid.cpp:60
+    o->max_cycle = 50;       // multigrid.cpp:94
+    o->smoother = 0;
+}
+
+// ---- gs.h mirror (reference layout, device pointers, null stream)
+int mgx_gauss_seidel(double *u, const double *rhs, long n, const double *v1, const double *v2,
+                     double k, double nu, double h) {
+    if (!u || !rhs || !v1 || !v2 || n < 2) return fail(MGX_E_ARG, "mgx_gauss_seidel: bad args");
+    mgx::Coef c = mgx::make_coef(k, nu, h);
+    mgx::launch_raw_gs_colour(u, rhs, v1, v2, n, c, 0, nullptr);
+    mgx::launch_raw_gs_colour(u, rhs, v1, v2, n, c, 1, nullptr);
+    return check_launch("mgx_gauss_seidel");
+}
+int mgx_residual(double *res, const double *u, const double *rhs, long n, const double *v1,
+                 const double *v2, double k, double nu, double h) {
+    if (!res || !u || !rhs || !v1 || !v2 || n < 2) return fail(MGX_E_ARG, "mgx_residual: bad args");
+    mgx::launch_raw_residual(res, u, rhs, v1, v2, n, mgx::make_coef(k, nu, h), nullptr);
+    return check_launch("mgx_residual");
+}
+int mgx_compute_norm(const double *res, long n, double *norm) {
+    if (!res || !norm || n < 1) return fail(MGX_E_ARG, "mgx_compute_norm: bad args");
+    std::lock_guard<std::mutex> g(g_raw_mu);
+    double *s = nullptr;
+    CHK(raw_scratch(&s));
+    double *out = s + mgx::norm_partials_size();
+    mgx::launch_norm(res, n, n + 1, s, out, nullptr);
+    CHK(check_launch("mgx_compute_norm"));
+    HIPCHK(hipMemcpy(norm, out, sizeof(double), hipMemcpyDeviceToHost));
+    return MGX_OK;
+}
+int mgx_prolongation(double *up, const double *u, long n) {
+    if (!up || !u || n < 1) return fail(MGX_E_ARG, "mgx_prolongation: bad args");
+    mgx::launch_raw_prolongation(up, u, n, nullptr);
+    return check_launch("mgx_prolongation");
+}
+int mgx_restriction(double *u, const double *up, long n) {
+    if (!u || !up || n < 2) return fail(MGX_E_ARG, "mgx_restriction: bad args");
+    mgx::launch_injection(u, n / 2 + 1, up, n + 1, n / 2 + 1, nullptr);
+    return check_launch("mgx_restriction");
+}
+int mgx_compute_rhs(double *rhs, const double *u, long n, const double *v1, const double *v2,
+                    double k, double nu, double h) {
+    if (!rhs || !u || !v1 || !v2 || n < 2) return fail(MGX_E_ARG, "mgx_compute_rhs: bad args");
+    mgx::launch_raw_rhs(rhs, u, v1, v2, n, mgx::make_coef(k, nu, h), nullptr);
+    return check_launch("mgx_compute_rhs");
+}
+
+// ---- context
+int mgx_create(mgx_ctx **out, long n, int maxlvl, double dt, double nu, const mgx_options *opt) {
+    if (!out) return fail(MGX_E_ARG, "mgx_create: null out");
+    *out = nullptr;
+    if (!is_pow2(n)) return fail(MGX_E_ARG, "mgx_create: n must be a power of two >= 2");
+    if (maxlvl < 1 || (n >> (maxlvl - 1)) < 2)
+        return fail(MGX_E_ARG, "mgx_create: maxlvl must satisfy 1 <= maxlvl, n>>(maxlvl-1) >= 2");
+    mgx_options o;
+    mgx_default_options(&o);
+    if (opt) o = *opt;
+    if (o.nsmooth < 0 || o.shape < 1 || o.coarse_maxit < 1 || o.max_cycle < 1)
+        return fail(MGX_E_ARG, "mgx_create: bad options");
+    mgx_ctx *c = new mgx_ctx();
+    c->N = n;
+    c->L = maxlvl;
+    c->dt = dt;
+    c->nu = nu;
+    c->opt = o;
+    auto bail = [&](int rc) {
+        free_ctx(c);
+        return rc;
+    };
+    if (o.device >= 0) {
+        hipError_t e = hipSetDevice(o.device);
+        if (e != hipSuccess) return bail(fail(MGX_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e)));
+    }
+    if (hipGetDevice(&c->device) != hipSuccess) return bail(fail(MGX_E_HIP, "hipGetDevice"));
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(MGX_E_HIP, "hipStreamCreate"));
+    c->lv.resize(maxlvl);
+    double h = 1.0 / n;   // dx (multigrid.cpp:194), doubled per level (:49)
+    for (int l = 0; l < maxlvl; ++l) {
+        Level &L = c->lv[l];
+        L.n = n >> l;
+        L.pitch = mgx::tower_pitch(L.n);
+        L.coef = mgx::make_coef(dt, nu, h);
+        h = 2 * h;
+        const size_t bytes = sizeof(double) * L.pitch * (L.n + 1);
+        double **bufs[5] = {&L.u[0], &L.u[1], &L.rhs, &L.v1, &L.v2};
+        for (double **b : bufs) {
+            if (hipMalloc(b, bytes) != hipSuccess)
+                return bail(fail(MGX_E_HIP, "hipMalloc (level tower): out of device memory"));
+            if (hipMemsetAsync(*b, 0, bytes, c->stream) != hipSuccess)
+                return bail(fail(MGX_E_HIP, "hipMemset"));
+        }
+    }
+    const size_t flat = sizeof(double) * (n + 1) * (n + 1);
+    if (hipMalloc(&c->partials, sizeof(double) * mgx::norm_partials_size()) != hipSuccess ||
+        hipMalloc(&c->dscal, sizeof(double) * 8) != hipSuccess ||
+        hipHostMalloc(&c->hscal, sizeof(double) * 8) != hipSuccess)
+        return bail(fail(MGX_E_HIP, "hipMalloc (scratch)"));
+    if (maxlvl > 1 && o.tower_mode == MGX_TOWER_REFERENCE) {
+        if (hipMalloc(&c->stage[0], flat) != hipSuccess || hipMalloc(&c->stage[1], flat) != hipSuccess)
+            return bail(fail(MGX_E_HIP, "hipMalloc (staging)"));
+    }
+    (void)hipMemsetAsync(c->dscal, 0, sizeof(double) * 8, c->stream);
+    memset(c->hscal, 0, sizeof(double) * 8);
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return bail(fail(MGX_E_HIP, "sync"));
+    *out = c;
+    return MGX_OK;
+}
+
+int mgx_destroy(mgx_ctx *c) {
+    free_ctx(c);
+    return MGX_OK;
+}
+
+static int upload_impl(mgx_ctx *c, const double *u0, const double *v1, const double *v2,
+                       hipMemcpyKind kind) {
+    if (!c || !u0 || !v1 || !v2) return fail(MGX_E_ARG, "mgx_upload: bad args");
+    HIPCHK(hipSetDevice(c->device));
+    Level &L = c->lv[0];
+    const size_t row = (c->N + 1) * sizeof(double);
+    L.cur = 0;
+    L.zero = false;
+    const double *src[3] = {u0, v1, v2};
+    double *dst[3] = {L.u[0], L.v1, L.v2};
+    for (int k = 0; k < 3; ++k)
+        HIPCHK(hipMemcpy2DAsync(dst[k], L.pitch * sizeof(double), src[k], row, row, c->N + 1,
+                                kind, c->stream));
+    for (int l = 1; l < c->L; ++l) {
+        c->lv[l].cur = 0;
+        c->lv[l].zero = false;
+    }
+    CHK(build_tower(c));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return MGX_OK;
+}
+
+int mgx_upload(mgx_ctx *c, const double *u0, const double *v1, const double *v2) {
+    return upload_impl(c, u0, v1, v2, hipMemcpyHostToDevice);
+}
+int mgx_upload_device(mgx_ctx *c, const double *u0, const double *v1, const double *v2) {
+    return upload_impl(c, u0, v1, v2, hipMemcpyDeviceToDevice);
+}
+
+static int download_impl(mgx_ctx *c, int level, int field, double *out, hipMemcpyKind kind) {
+    if (!c || !out || level < 0 || level >= c->L || field < 0 || field > 3)
+        return fail(MGX_E_ARG, "mgx_download: bad args");
+    HIPCHK(hipSetDevice(c->device));
+    CHK(materialize(c, level));
+    Level &L = c->lv[level];
+    const double *src = field == 0 ? L.U() : field == 1 ? L.rhs : field == 2 ? L.v1 : L.v2;
+    const size_t row = (L.n + 1) * sizeof(double);
+    HIPCHK(hipMemcpy2DAsync(out, row, src, L.pitch * sizeof(double), row, L.n + 1, kind,
+                            c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return MGX_OK;
+}
+
+int mgx_download(mgx_ctx *c, double *u) { return download_impl(c, 0, 0, u, hipMemcpyDeviceToHost); }
+int mgx_download_device(mgx_ctx *c, double *u) {
+    return download_impl(c, 0, 0, u, hipMemcpyDeviceToDevice);
+}
+int mgx_download_level(mgx_ctx *c, int level, int field, double *out) {
+    return download_impl(c, level, field, out, hipMemcpyDeviceToHost);
+}
+
+int mgx_rhs(mgx_ctx *c) {
+    if (!c) return fail(MGX_E_ARG, "null ctx");
+    return op_rhs(c);
+}
+int mgx_gs(mgx_ctx *c, int level, int sweeps) {
+    if (!c || level < 0 || level >= c->L || sweeps < 0) return fail(MGX_E_ARG, "mgx_gs: bad args");
+    return op_gs(c, level, sweeps);
+}
+int mgx_residual_norm(mgx_ctx *c, int level, double *norm) {
+    if (!c || level < 0 || level >= c->L || !norm) return fail(MGX_E_ARG, "mgx_residual_norm: bad args");
+    return op_residual_norm(c, level, norm);
+}
+int mgx_restrict(mgx_ctx *c, int level) {
+    if (!c || level < 0 || level >= c->L - 1) return fail(MGX_E_ARG, "mgx_restrict: bad level");
+    return op_restrict(c, level);
+}
+int mgx_prolong_add(mgx_ctx *c, int level) {
+    if (!c || level < 0 || level >= c->L - 1) return fail(MGX_E_ARG, "mgx_prolong_add: bad level");
+    return op_prolong_add(c, level);
+}
+int mgx_vcycle(mgx_ctx *c) {
+    if (!c) return fail(MGX_E_ARG, "null ctx");
+    return op_vcycle(c, 0);
+}
+int mgx_mg_outer(mgx_ctx *c, double tol, int *cycles, double *res0, double *res) {
+    if (!c) return fail(MGX_E_ARG, "null ctx");
+    return op_mg_outer(c, tol, cycles, res0, res);
+}
+int mgx_step(mgx_ctx *c, double tol, int *cycles) {
+    if (!c) return fail(MGX_E_ARG, "null ctx");
+    CHK(op_rhs(c));
+    return op_mg_outer(c, tol, cycles, nullptr, nullptr);
+}
+int mgx_run_cycles(mgx_ctx *c, int cycles, double *res) {
+    if (!c || cycles < 0) return fail(MGX_E_ARG, "mgx_run_cycles: bad args");
+    double r = 0;
+    for (int k = 0; k < cycles; ++k) {
+        CHK(op_vcycle(c, 0));
+        CHK(op_residual_norm(c, 0, &r));
+    }
+    if (res) *res = r;
+    return MGX_OK;
+}
+
+int mgx_level_n(mgx_ctx *c, int level, long *n) {
+    if (!c || !n || level < 0 || level >= c->L) return fail(MGX_E_ARG, "mgx_level_n: bad args");
+    *n = c->lv[level].n;
+    return MGX_OK;
+}
+int mgx_coarse_iterations(mgx_ctx *c, long *iters) {
+    if (!c || !iters) return fail(MGX_E_ARG, "bad args");
+    HIPCHK(hipMemcpyAsync(c->hscal + 2, c->dscal + 2, 2 * sizeof(double), hipMemcpyDeviceToHost,
+                          c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    *iters = (long)(c->hscal[2] + c->hscal[4]);
+    return MGX_OK;
+}
+int mgx_stream(mgx_ctx *c, void **stream) {
+    if (!c || !stream) return fail(MGX_E_ARG, "bad args");
+    *stream = (void *)c->stream;
+    return MGX_OK;
+}
+int mgx_synchronize(mgx_ctx *c) {
+    if (!c) return fail(MGX_E_ARG, "null ctx");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return MGX_OK;
+}
+
+int mgx_profile_enable(mgx_ctx *c, int on) {
+    if (!c) return fail(MGX_E_ARG, "null ctx");
+    CHK(prof_flush(c));
+    c->prof = on != 0;
+    return MGX_OK;
+}
+int mgx_profile_reset(mgx_ctx *c) {
+    if (!c) return fail(MGX_E_ARG, "null ctx");
+    CHK(prof_flush(c));
+    memset(c->sum_ms, 0, sizeof(c->sum_ms));
+    memset(c->sum_bytes, 0, sizeof(c->sum_bytes));
+    memset(c->count, 0, sizeof(c->count));
+    return MGX_OK;
+}
+int mgx_profile_get(mgx_ctx *c, int kind, int level, long *launches, double *ms, double *bytes) {
+    if (!c || kind < 0 || kind >= MGX_K_COUNT || level >= 64)
+        return fail(MGX_E_ARG, "mgx_profile_get: bad args");
+    CHK(prof_flush(c));
+    long n = 0;
+    double t = 0, b = 0;
+    for (int l = 0; l < 64; ++l) {
+        if (level >= 0 && l != level) continue;
+        n += c->count[kind][l];
+        t += c->sum_ms[kind][l];
+        b += c->sum_bytes[kind][l];
+    }
+    if (launches) *launches = n;
+    if (ms) *ms = t;
+    if (bytes) *bytes = b;
+    return MGX_OK;
+}
+
+// ---- timestepper (multigrid.cpp:124-186)
+int mgx_timestepper_ex(double *uT, const double *u0, const double *v1, const double *v2,
+                       double nu, int maxlvl, long n, double dt, double T, double dx, double tol,
+                       const mgx_options *opt, int *cycles_per_step) {
+    (void)dx;   // the context derives dx = 1/n (multigrid.cpp:194)
+    if (!uT || !u0 || !v1 || !v2) return fail(MGX_E_ARG, "mgx_timestepper: null array");
+    mgx_ctx *c = nullptr;
+    CHK(mgx_create(&c, n, maxlvl, dt, nu, opt));
+    int rc = mgx_upload(c, u0, v1, v2);
+    const int steps = (int)(T / dt);   // multigrid.cpp:165
+    for (int it = 0; rc == MGX_OK && it < steps; ++it) {
+        int cyc = 0;
+        rc = mgx_step(c, tol, &cyc);
+        if (rc == MGX_E_NOCONV) {
+            // multigrid.cpp:117-119 only warns; keep stepping
+            printf("multigrid did not converge in %d cycles\n", c->opt.max_cycle);
+            rc = MGX_OK;
+        }
+        if (cycles_per_step) cycles_per_step[it] = cyc;
+    }
+    if (rc == MGX_OK) rc = mgx_download(c, uT);
+    std::string keep = g_err;
+    mgx_destroy(c);
+    g_err = keep;
+    return rc;
+}
+
+int mgx_timestepper(double *uT, const double *u0, const double *v1, const double *v2, double nu,
+                    int maxlvl, long n, double dt, double T, double dx, double tol, int shape) {
+    mgx_options o;
+    mgx_default_options(&o);
+    o.shape = shape;
+    return mgx_timestepper_ex(uT, u0, v1, v2, nu, maxlvl, n, dt, T, dx, tol, &o, nullptr);
+}
+
+}  // extern "C"
+
+// ---- reference problem setup (multigrid.cpp:206-233), host, glibc libm
+#include <thread>
+extern "C" int mgx_init_problem(double *u0, double *v1, double *v2, long N, int nthreads) {
+    if (!u0 || !v1 || !v2 || N < 1) return fail(MGX_E_ARG, "mgx_init_problem: bad args");
+    const double PI = 3.1415926535897932;   // multigrid.cpp:14
+    const double dx = 1.0 / N;
+    const double x0 = 0.2, y0 = 0.4, sigma = 100.0, kx = 1.0 * PI, ky = 1.0 * PI;
+    const long w = N + 1;
+    int nt = nthreads > 0 ? nthreads : (int)std::thread::hardware_concurrency();
+    if (nt < 1) nt = 1;
+    if (nt > w) nt = (int)w;
+    auto rows = [&](long r0, long r1) {
+        for (long i = r0; i < r1; ++i) {
+            const double xi = (double)i;
+            for (long j = 0; j < w; ++j) {
+                const double yj = (double)j;
+                u0[i * w + j] = std::exp(-sigma * ((xi * dx - x0) * (xi * dx - x0) +
+                                                   (yj * dx - y0) * (yj * dx - y0)));
+                v1[i * w + j] = -ky * std::sin(kx * xi * dx) * std::cos(ky * yj * dx);
+                v2[i * w + j] = kx * std::cos(kx * xi * dx) * std::sin(ky * yj * dx);
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    const long per = (w + nt - 1) / nt;
+    for (int t = 0; t < nt; ++t) {
+        long r0 = t * per, r1 = std::min(w, r0 + per);
+        if (r0 < r1) th.emplace_back(rows, r0, r1);
+    }
+    for (auto &x : th) x.join();
+    for (long i = 0; i < N; ++i) {   // zero boundary, multigrid.cpp:227-233
+        u0[i] = 0.0;
+        u0[i * w + N] = 0.0;
+        u0[N * w + i + 1] = 0.0;
+        u0[i * w] = 0.0;
+    }
+    return MGX_OK;
+}

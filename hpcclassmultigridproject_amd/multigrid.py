@@ -1,0 +1,178 @@
+"""Solver-level mirror of the reference's multigrid.cpp on the MI355X path.
+
+* ``init_problem(N)``  -- multigrid.cpp:206-233 (host, glibc libm, bitwise inputs)
+* ``timestepper(...)`` -- multigrid.cpp:124-186, same signature; host numpy arrays
+* ``Multigrid``        -- the level towers resident in HBM (multigrid.cpp:131-162)
+  with ``mg_inner()`` (multigrid.cpp:17-92, one V/W-cycle), ``mg_outer()``
+  (multigrid.cpp:97-120), ``step()`` (one timestep, :165-172) and the op-level
+  pieces ``gs``, ``residual_norm``, ``restrict``, ``prolong_add``, ``rhs``.
+
+All compute runs in libmgx.so on the GPU; this module only marshals arguments.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, default_options, lib
+
+
+def _np_ptr(a: np.ndarray):
+    if a.dtype != np.float64 or not a.flags["C_CONTIGUOUS"]:
+        raise ValueError("expected a C-contiguous float64 array")
+    return a.ctypes.data
+
+
+def default_maxlvl(N: int) -> int:
+    """multigrid.cpp:193: int(log2(N)) - 4 (coarsest n = 16... solved by GS)."""
+    return int(math.log2(N)) - 4
+
+
+def init_problem(N: int, nthreads: int = 0):
+    """multigrid.cpp:206-233 -> (u0, v1, v2), each (N+1)^2 float64."""
+    cnt = (N + 1) * (N + 1)
+    u0, v1, v2 = (np.empty(cnt, dtype=np.float64) for _ in range(3))
+    check(lib().mgx_init_problem(_np_ptr(u0), _np_ptr(v1), _np_ptr(v2), N, nthreads))
+    return u0, v1, v2
+
+
+def timestepper(uT, u0, v1, v2, nu, maxlvl, n, dt, T, dx, tol, shape=1, *, nsmooth=3,
+                tower_mode=_lib.TOWER_REFERENCE, device=-1):
+    """multigrid.cpp:124 -- run (int)(T/dt) CN steps; writes uT, returns cycles per step."""
+    steps = int(T / dt)
+    cyc = (C.c_int * max(steps, 1))()
+    opt = default_options(shape=shape, nsmooth=nsmooth, tower_mode=tower_mode, device=device)
+    check(lib().mgx_timestepper_ex(_np_ptr(uT), _np_ptr(u0), _np_ptr(v1), _np_ptr(v2), nu,
+                                   maxlvl, n, dt, T, dx, tol, C.byref(opt), cyc))
+    return list(cyc)[:steps]
+
+
+class Multigrid:
+    """Device-resident level towers and the V-cycle (mgx_ctx)."""
+
+    def __init__(self, N, maxlvl, dt, nu, *, nsmooth=3, shape=1,
+                 tower_mode=_lib.TOWER_REFERENCE, device=-1, smoother=0, coarse_tol=1e-5,
+                 coarse_maxit=1000, max_cycle=50):
+        self.N, self.maxlvl, self.dt, self.nu = N, maxlvl, dt, nu
+        self.opt = default_options(nsmooth=nsmooth, shape=shape, tower_mode=tower_mode,
+                                   device=device, smoother=smoother, coarse_tol=coarse_tol,
+                                   coarse_maxit=coarse_maxit, max_cycle=max_cycle)
+        h = C.c_void_p()
+        check(lib().mgx_create(C.byref(h), N, maxlvl, dt, nu, C.byref(self.opt)))
+        self._h = h
+
+    # -- lifetime
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().mgx_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    # -- data
+    def upload(self, u0, v1, v2):
+        if isinstance(u0, np.ndarray):
+            check(lib().mgx_upload(self._h, _np_ptr(u0), _np_ptr(v1), _np_ptr(v2)))
+        else:   # device tensors in the reference layout
+            check(lib().mgx_upload_device(self._h, u0.data_ptr(), v1.data_ptr(),
+                                          v2.data_ptr()))
+
+    def download(self, out=None):
+        out = np.empty((self.N + 1) ** 2, dtype=np.float64) if out is None else out
+        check(lib().mgx_download(self._h, _np_ptr(out)))
+        return out
+
+    def level_n(self, level):
+        n = C.c_long()
+        check(lib().mgx_level_n(self._h, level, C.byref(n)))
+        return n.value
+
+    def download_level(self, level, field="u"):
+        f = {"u": 0, "rhs": 1, "v1": 2, "v2": 3}[field]
+        n = self.level_n(level)
+        out = np.empty((n + 1) ** 2, dtype=np.float64)
+        check(lib().mgx_download_level(self._h, level, f, _np_ptr(out)))
+        return out
+
+    # -- ops (multigrid.cpp call sites)
+    def rhs(self):
+        check(lib().mgx_rhs(self._h))
+
+    def gs(self, level, sweeps=1):
+        check(lib().mgx_gs(self._h, level, sweeps))
+
+    def residual_norm(self, level=0):
+        r = C.c_double()
+        check(lib().mgx_residual_norm(self._h, level, C.byref(r)))
+        return r.value
+
+    def restrict(self, level):
+        check(lib().mgx_restrict(self._h, level))
+
+    def prolong_add(self, level):
+        check(lib().mgx_prolong_add(self._h, level))
+
+    def mg_inner(self):
+        """multigrid.cpp:17 at lvl=0: one V (shape=1) or W (shape=2) cycle."""
+        check(lib().mgx_vcycle(self._h))
+
+    vcycle = mg_inner
+
+    def mg_outer(self, tol=1e-6):
+        """multigrid.cpp:97 -> (cycles, res0, res); cap hit is reported, not raised."""
+        cyc, r0, r = C.c_int(), C.c_double(), C.c_double()
+        rc = check(lib().mgx_mg_outer(self._h, tol, C.byref(cyc), C.byref(r0), C.byref(r)),
+                   allow=(_lib.MGX_E_NOCONV,))
+        return cyc.value, r0.value, r.value, rc == _lib.MGX_E_NOCONV
+
+    def step(self, tol=1e-6):
+        cyc = C.c_int()
+        check(lib().mgx_step(self._h, tol, C.byref(cyc)), allow=(_lib.MGX_E_NOCONV,))
+        return cyc.value
+
+    def run_cycles(self, cycles):
+        r = C.c_double()
+        check(lib().mgx_run_cycles(self._h, cycles, C.byref(r)))
+        return r.value
+
+    def coarse_iterations(self):
+        it = C.c_long()
+        check(lib().mgx_coarse_iterations(self._h, C.byref(it)))
+        return it.value
+
+    def synchronize(self):
+        check(lib().mgx_synchronize(self._h))
+
+    def stream(self):
+        s = C.c_void_p()
+        check(lib().mgx_stream(self._h, C.byref(s)))
+        return s.value
+
+    # -- profiling (HIP events on the context stream)
+    def profile(self, on=True):
+        check(lib().mgx_profile_enable(self._h, 1 if on else 0))
+
+    def profile_reset(self):
+        check(lib().mgx_profile_reset(self._h))
+
+    def profile_get(self, kind, level=-1):
+        n, ms, b = C.c_long(), C.c_double(), C.c_double()
+        check(lib().mgx_profile_get(self._h, kind, level, C.byref(n), C.byref(ms), C.byref(b)))
+        return n.value, ms.value, b.value

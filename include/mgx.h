@@ -1,0 +1,171 @@
+/* mgx.h -- C ABI of the MI355X-native geometric-multigrid V-cycle (libmgx.so).
+ *
+ * Drop-in boundary for the reference's hot path (soniareilly/HPCClassMultigridProject):
+ *   - the op-level seam gs.h:3-17 (gauss_seidel, residual, compute_norm,
+ *     prolongation, restriction, compute_rhs), here on DEVICE pointers in the
+ *     reference layout (row-major (n+1)^2 doubles, element (i,j) at i*(n+1)+j);
+ *   - the solver-level functions multigrid.cpp:17 (mg_inner), :97 (mg_outer)
+ *     and :124 (timestepper), here on a context that keeps the level towers
+ *     resident in HBM (mgx_ctx), plus mgx_timestepper with the exact reference
+ *     signature on HOST arrays.
+ *
+ * Conventions:
+ *   - every function returns 0 on success and a non-zero MGX_E* code on
+ *     failure; mgx_last_error() returns the message of the last failure on the
+ *     calling thread;
+ *   - the caller owns every buffer passed in; ops never allocate;
+ *   - raw-pointer ops run on the HIP null stream and are ordered with other
+ *     null-stream work; mgx_compute_norm synchronises (it returns a host value,
+ *     like gs.cpp:86).  Context functions run on the context's own stream;
+ *   - all arithmetic is fp64 with the reference's term order and no FMA
+ *     contraction, so op results are bitwise equal to the serial reference.
+ */
+#ifndef MGX_H
+#define MGX_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MGX_OK 0
+#define MGX_E_ARG 1     /* invalid argument (sizes, level, null pointer) */
+#define MGX_E_HIP 2     /* a HIP runtime call failed */
+#define MGX_E_RCCL 3    /* an RCCL call failed */
+#define MGX_E_NOCONV 4  /* mg_outer hit its cycle cap (reported, not fatal) */
+
+const char *mgx_last_error(void);
+int mgx_version(void);
+
+/* ---------------------------------------------------------------------------
+ * Op-level seam: replaces gs.h (reference gs.h:3-17, implementations gs.cpp).
+ * Device pointers, reference layout.  k = dt, h = grid spacing at this level.
+ * ------------------------------------------------------------------------- */
+
+/* gs.h:9 / gs.cpp:109-189: one red-black Gauss-Seidel sweep, in place. */
+int mgx_gauss_seidel(double *u, const double *rhs, long n, const double *v1,
+                     const double *v2, double k, double nu, double h);
+/* gs.h:3 / gs.cpp:55-83: res = rhs - A u on the interior; res boundary untouched. */
+int mgx_residual(double *res, const double *u, const double *rhs, long n,
+                 const double *v1, const double *v2, double k, double nu, double h);
+/* gs.h:5 / gs.cpp:86-107: *norm = sqrt(sum of interior res^2).  Does not modify res. */
+int mgx_compute_norm(const double *res, long n, double *norm);
+/* gs.h:16 / gs.cpp:228-266: bilinear prolongation, up (2n+1)^2 <- u (n+1)^2. */
+int mgx_prolongation(double *up, const double *u, long n);
+/* gs.h:17 / gs.cpp:268-292: injection, u (n/2+1)^2 <- up (n+1)^2 (incl. boundary). */
+int mgx_restriction(double *u, const double *up, long n);
+/* gs.h:13 / gs.cpp:24-53: Crank-Nicolson right-hand side B u on the interior. */
+int mgx_compute_rhs(double *rhs, const double *u, long n, const double *v1,
+                    const double *v2, double k, double nu, double h);
+
+/* multigrid.cpp:206-233: the reference problem on the host with the C library
+ * (glibc) exp/sin/cos, so inputs are bitwise those of the reference: Gaussian
+ * u0 (x0=.2, y0=.4, sigma=100) with zero boundary, v1 = -pi sin(pi x) cos(pi y),
+ * v2 = pi cos(pi x) sin(pi y); x = i/N, y = j/N.  Arrays of (N+1)^2 doubles.
+ * nthreads <= 0: all hardware threads. */
+int mgx_init_problem(double *u0, double *v1, double *v2, long N, int nthreads);
+
+/* ---------------------------------------------------------------------------
+ * Solver level.
+ * ------------------------------------------------------------------------- */
+
+/* Tower construction (multigrid.cpp:148-160). */
+#define MGX_TOWER_REFERENCE 0 /* bitwise reference semantics (index quirk, zero fill) */
+#define MGX_TOWER_CORRECT 1   /* every level injected from the level above */
+
+typedef struct mgx_options {
+    int nsmooth;        /* RB-GS sweeps before and after the coarse correction
+                           (NITER, multigrid.cpp:41; reference 3) */
+    int shape;          /* 1 = V-cycle, 2 = W-cycle (multigrid.cpp:52) */
+    int tower_mode;     /* MGX_TOWER_* (default REFERENCE) */
+    int device;         /* HIP device ordinal for this context */
+    double coarse_tol;  /* coarsest-level GS stop, absolute (multigrid.cpp:60: 1e-5) */
+    int coarse_maxit;   /* coarsest-level GS cap (multigrid.cpp:60: 1000) */
+    int max_cycle;      /* mg_outer cycle cap (multigrid.cpp:94: 50) */
+    int smoother;       /* 0 = fused one-pass RB sweep (default), 1 = two colour passes */
+} mgx_options;
+
+/* Fills *opt with the reference defaults. */
+void mgx_default_options(mgx_options *opt);
+
+/* multigrid.cpp:124-186 with the reference signature: host arrays u0, v1, v2
+ * of (n+1)^2 doubles in, uT out.  Runs (int)(T/dt) Crank-Nicolson steps, each
+ * compute_rhs + mg_outer, entirely on the GPU. */
+int mgx_timestepper(double *uT, const double *u0, const double *v1, const double *v2,
+                    double nu, int maxlvl, long n, double dt, double T, double dx,
+                    double tol, int shape);
+/* Same with options; cycles_per_step (may be NULL) gets mg_outer's cycle count
+ * for every step (length (int)(T/dt)). */
+int mgx_timestepper_ex(double *uT, const double *u0, const double *v1, const double *v2,
+                       double nu, int maxlvl, long n, double dt, double T, double dx,
+                       double tol, const mgx_options *opt, int *cycles_per_step);
+
+/* Context: the level towers u/rhs/v1/v2 (multigrid.cpp:131-162) resident in HBM.
+ * n = finest N (power of two), maxlvl = number of levels, dt, nu as in
+ * timestepper.  Multi-GPU: see mgx_create_dist. */
+typedef struct mgx_ctx mgx_ctx;
+
+int mgx_create(mgx_ctx **ctx, long n, int maxlvl, double dt, double nu,
+               const mgx_options *opt);
+int mgx_destroy(mgx_ctx *ctx);
+
+/* Host <-> device in the reference layout ((n+1)^2 row-major).  upload sets
+ * u = u0, v1, v2 on the finest level and builds the coarse velocity tower;
+ * download copies the finest u. */
+int mgx_upload(mgx_ctx *ctx, const double *u0, const double *v1, const double *v2);
+int mgx_download(mgx_ctx *ctx, double *u);
+/* Device-pointer variants (reference layout, device memory). */
+int mgx_upload_device(mgx_ctx *ctx, const double *u0, const double *v1, const double *v2);
+int mgx_download_device(mgx_ctx *ctx, double *u);
+
+/* compute_rhs on the finest level (multigrid.cpp:167). */
+int mgx_rhs(mgx_ctx *ctx);
+/* `sweeps` RB-GS sweeps on level `level` (gauss_seidel, multigrid.cpp:69-72). */
+int mgx_gs(mgx_ctx *ctx, int level, int sweeps);
+/* residual + compute_norm on `level` (multigrid.cpp:104-105, 62-63). */
+int mgx_residual_norm(mgx_ctx *ctx, int level, double *norm);
+/* residual on `level` restricted into rhs[level+1], and u[level+1] = 0
+ * (multigrid.cpp:73-77). */
+int mgx_restrict(mgx_ctx *ctx, int level);
+/* u[level] += prolongation(u[level+1]) (multigrid.cpp:81-83). */
+int mgx_prolong_add(mgx_ctx *ctx, int level);
+/* One V- (or W-) cycle from the finest level: mg_inner(lvl=0) (multigrid.cpp:17-92). */
+int mgx_vcycle(mgx_ctx *ctx);
+/* mg_outer (multigrid.cpp:97-120): cycles until ||r||/||r0|| <= tol or the cap.
+ * Any output pointer may be NULL.  Returns MGX_E_NOCONV when the cap is hit. */
+int mgx_mg_outer(mgx_ctx *ctx, double tol, int *cycles, double *res0, double *res);
+/* One timestep: mgx_rhs + mgx_mg_outer (multigrid.cpp:165-172). */
+int mgx_step(mgx_ctx *ctx, double tol, int *cycles);
+/* Bench step x `cycles`: V-cycle + residual + norm, no tolerance stop.
+ * *res (may be NULL) receives the last residual norm. */
+int mgx_run_cycles(mgx_ctx *ctx, int cycles, double *res);
+
+/* Introspection. */
+int mgx_level_n(mgx_ctx *ctx, int level, long *n);
+/* Copy level `level`'s field (0=u, 1=rhs, 2=v1, 3=v2) to host, reference layout. */
+int mgx_download_level(mgx_ctx *ctx, int level, int field, double *out);
+/* Number of coarsest-level GS iterations performed since creation. */
+int mgx_coarse_iterations(mgx_ctx *ctx, long *iters);
+/* The HIP stream (hipStream_t) the context launches on. */
+int mgx_stream(mgx_ctx *ctx, void **stream);
+int mgx_synchronize(mgx_ctx *ctx);
+
+/* Per-kernel timing with HIP events on the context stream. */
+#define MGX_K_GS 0             /* RB-GS sweep (one full red+black sweep) */
+#define MGX_K_RESTRICT 1       /* residual restricted to the coarse rhs */
+#define MGX_K_PROLONG 2        /* prolongation + add */
+#define MGX_K_RESNORM 3        /* residual + norm partials */
+#define MGX_K_COARSE 4         /* coarsest-level solve */
+#define MGX_K_RHS 5            /* compute_rhs */
+#define MGX_K_HALO 6           /* halo exchange (multi-GPU) */
+#define MGX_K_COUNT 7
+int mgx_profile_enable(mgx_ctx *ctx, int on);
+int mgx_profile_reset(mgx_ctx *ctx);
+/* For kernel kind `kind` on level `level` (-1 = all levels): launches, summed
+ * device milliseconds, summed algorithmic bytes (SURVEY 8d byte model). */
+int mgx_profile_get(mgx_ctx *ctx, int kind, int level, long *launches, double *ms,
+                    double *bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MGX_H */

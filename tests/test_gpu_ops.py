@@ -1,0 +1,159 @@
+"""GPU parity of the op-level seam (gs.h mirror) and the context ops.
+
+Bar: BITWISE equality with the reference's own outputs (golden fixtures) and
+with the CPU checker -- every kernel evaluates the reference's expressions term
+by term with no FMA contraction.  The one exception is compute_norm, whose
+summation order differs (a deterministic tree instead of a serial loop):
+tolerance 1e-13 relative, stated here.
+"""
+import numpy as np
+import pytest
+import torch
+from conftest import load_golden
+
+from hpcclassmultigridproject_amd import Multigrid, gs, init_problem
+
+pytestmark = pytest.mark.gpu
+NORM_RTOL = 1e-13
+DEV = "cuda:0"
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def host(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+@pytest.mark.parametrize("N", [8, 16, 32, 64])
+def test_raw_ops_bitwise_vs_reference_fixture(N):
+    g = load_golden(f"ops_N{N}.npz")
+    _, k, nu, h = g["params"]
+    u, rhs, v1, v2 = dev(g["u"]), dev(g["rhs"]), dev(g["v1"]), dev(g["v2"])
+    w = u.clone()
+    gs.gauss_seidel(w, rhs, N, v1, v2, k, nu, h)
+    assert np.array_equal(host(w), g["gs"])
+    res = torch.zeros_like(u)
+    gs.residual(res, u, rhs, N, v1, v2, k, nu, h)
+    assert np.array_equal(host(res), g["res"])
+    assert abs(gs.compute_norm(res, N) - g["norm"][0]) <= NORM_RTOL * g["norm"][0]
+    cr = torch.zeros_like(u)
+    gs.compute_rhs(cr, u, N, v1, v2, k, nu, h)
+    assert np.array_equal(host(cr), g["crhs"])
+    up = torch.zeros((2 * N + 1) ** 2, dtype=torch.float64, device=DEV)
+    gs.prolongation(up, u, N)
+    assert np.array_equal(host(up), g["prol"])
+    rs = torch.zeros((N // 2 + 1) ** 2, dtype=torch.float64, device=DEV)
+    gs.restriction(rs, u, N)
+    assert np.array_equal(host(rs), g["restr"])
+
+
+@pytest.mark.parametrize("N", [2, 4, 6, 130, 1000])
+def test_raw_ops_bitwise_vs_oracle_odd_sizes(oracle_mod, N):
+    O = oracle_mod
+    rng = np.random.default_rng(N)
+    cnt = (N + 1) ** 2
+    u, rhs, v1, v2 = (rng.uniform(-2, 2, cnt) for _ in range(4))
+    k, nu, h = 0.1 / N, -0.01, 1.0 / N
+    du, drhs, dv1, dv2 = dev(u), dev(rhs), dev(v1), dev(v2)
+    gs.gauss_seidel(du, drhs, N, dv1, dv2, k, nu, h)
+    assert np.array_equal(host(du), O.gauss_seidel(u.copy(), rhs, N, v1, v2, k, nu, h))
+    res = torch.zeros_like(du)
+    gs.residual(res, dev(u), drhs, N, dv1, dv2, k, nu, h)
+    ref = O.residual(u, rhs, N, v1, v2, k, nu, h)
+    assert np.array_equal(host(res), ref)
+    nr = O.compute_norm(ref, N)
+    assert abs(gs.compute_norm(res, N) - nr) <= NORM_RTOL * nr
+    up = torch.zeros((2 * N + 1) ** 2, dtype=torch.float64, device=DEV)
+    gs.prolongation(up, dev(u), N)
+    assert np.array_equal(host(up), O.prolongation(u, N))
+    if N % 2 == 0:
+        rs = torch.zeros((N // 2 + 1) ** 2, dtype=torch.float64, device=DEV)
+        gs.restriction(rs, dev(u), N)
+        assert np.array_equal(host(rs), O.restriction(u, N))
+
+
+def _level_setup(O, N, maxlvl, tower_mode=0, nu=-4e-4):
+    u0, v1, v2 = init_problem(N)
+    dt = 1.0 / N / 10
+    t = O.Tower(u0, v1, v2, N, maxlvl, tower_mode)
+    O.compute_rhs(t.ufine, N, v1, v2, dt, nu, 1.0 / N, rhs=t.rhsfine)
+    return u0, v1, v2, dt, t
+
+
+@pytest.mark.parametrize("tower_mode", [0, 1])
+def test_context_tower_matches_oracle(oracle_mod, tower_mode):
+    O = oracle_mod
+    N, L = 256, 5
+    u0, v1, v2, dt, t = _level_setup(O, N, L, tower_mode)
+    with Multigrid(N, L, dt, -4e-4, tower_mode=tower_mode) as mg:
+        mg.upload(u0, v1, v2)
+        for l in range(L):
+            n = N >> l
+            for f in ("v1", "v2"):
+                assert np.array_equal(mg.download_level(l, f), t.level(f, l)[: (n + 1) ** 2]), (l, f)
+
+
+@pytest.mark.parametrize("smoother", [0, 1])
+@pytest.mark.parametrize("N", [16, 128, 512, 4096])
+def test_context_gs_bitwise_vs_oracle(oracle_mod, N, smoother):
+    """One-pass fused RB sweep (0) and two-colour passes (1) == gs.cpp:109."""
+    O = oracle_mod
+    u0, v1, v2 = init_problem(N)
+    dt, nu = 1.0 / N / 10, -4e-4
+    with Multigrid(N, 1, dt, nu, smoother=smoother) as mg:
+        mg.upload(u0, v1, v2)
+        mg.rhs()
+        rhs = O.compute_rhs(u0, N, v1, v2, dt, nu, 1.0 / N)
+        mg.gs(0, 3)
+        ref = u0.copy()
+        for _ in range(3):
+            O.gauss_seidel(ref, rhs, N, v1, v2, dt, nu, 1.0 / N)
+        assert np.array_equal(mg.download(), ref)
+
+
+def test_context_rhs_residual_norm_vs_oracle(oracle_mod):
+    O = oracle_mod
+    N = 1024
+    u0, v1, v2 = init_problem(N)
+    dt, nu = 1.0 / N / 10, -4e-4
+    with Multigrid(N, 1, dt, nu) as mg:
+        mg.upload(u0, v1, v2)
+        mg.rhs()
+        rhs = O.compute_rhs(u0, N, v1, v2, dt, nu, 1.0 / N)
+        got = mg.download_level(0, "rhs").reshape(N + 1, N + 1)
+        assert np.array_equal(got[1:N, 1:N], rhs.reshape(N + 1, N + 1)[1:N, 1:N])
+        mg.gs(0, 1)
+        u = u0.copy()
+        O.gauss_seidel(u, rhs, N, v1, v2, dt, nu, 1.0 / N)
+        r = O.compute_norm(O.residual(u, rhs, N, v1, v2, dt, nu, 1.0 / N), N)
+        assert abs(mg.residual_norm(0) - r) <= NORM_RTOL * r
+
+
+def test_context_restrict_prolong_vs_oracle(oracle_mod):
+    O = oracle_mod
+    N, L = 512, 3
+    u0, v1, v2, dt, t = _level_setup(O, N, L)
+    nu = -4e-4
+    with Multigrid(N, L, dt, nu) as mg:
+        mg.upload(u0, v1, v2)
+        mg.rhs()
+        mg.gs(0, 2)
+        mg.restrict(0)
+        u = u0.copy()
+        rhs = t.rhsfine
+        for _ in range(2):
+            O.gauss_seidel(u, rhs, N, v1, v2, dt, nu, 1.0 / N)
+        res = O.residual(u, rhs, N, v1, v2, dt, nu, 1.0 / N)
+        rc = O.restriction(res, N).reshape(N // 2 + 1, N // 2 + 1)
+        got = mg.download_level(1, "rhs").reshape(N // 2 + 1, N // 2 + 1)
+        assert np.array_equal(got[1:-1, 1:-1], rc[1:-1, 1:-1])
+        # coarse u is zero after restrict (multigrid.cpp:77)
+        assert not mg.download_level(1, "u").any()
+        mg.gs(1, 1)   # gives u[1] content
+        uc = mg.download_level(1, "u")
+        mg.prolong_add(0)
+        ref = u + O.prolongation(uc, N // 2)
+        assert np.array_equal(mg.download(), ref)
