@@ -15,10 +15,10 @@ HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "mgx.h")
 
 MGX_OK, MGX_E_ARG, MGX_E_HIP, MGX_E_RCCL, MGX_E_NOCONV = 0, 1, 2, 3, 4
 TOWER_REFERENCE, TOWER_CORRECT = 0, 1
-K_GS, K_RESTRICT, K_PROLONG, K_RESNORM, K_COARSE, K_RHS, K_HALO = range(7)
+K_GS, K_RESTRICT, K_PROLONG, K_RESNORM, K_COARSE, K_RHS, K_HALO, K_PSMOOTH = range(8)
 KERNEL_NAMES = {K_GS: "gs_sweep", K_RESTRICT: "residual_restrict", K_PROLONG: "prolong_add",
                 K_RESNORM: "residual_norm", K_COARSE: "coarse_solve", K_RHS: "compute_rhs",
-                K_HALO: "halo_exchange"}
+                K_HALO: "halo_exchange", K_PSMOOTH: "prolong_smooth"}
 
 
 class MGXError(RuntimeError):
@@ -31,7 +31,7 @@ class Options(C.Structure):
     """mgx_options (include/mgx.h)."""
     _fields_ = [("nsmooth", C.c_int), ("shape", C.c_int), ("tower_mode", C.c_int),
                 ("device", C.c_int), ("coarse_tol", C.c_double), ("coarse_maxit", C.c_int),
-                ("max_cycle", C.c_int), ("smoother", C.c_int)]
+                ("max_cycle", C.c_int), ("smoother", C.c_int), ("fuse", C.c_int)]
 
 
 _dp = C.POINTER(C.c_double)

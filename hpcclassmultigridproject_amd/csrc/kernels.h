@@ -46,6 +46,13 @@ void launch_norm(const double *res, long n, long pitch, double *partials, double
 void launch_gs_sweep(const double *uin, double *uout, const double *rhs, const double *v1,
                      const double *v2, long n, long pitch, Coef c, bool zero_in,
                      hipStream_t s);
+// `sweeps` (1..3) red-black sweeps in one pass, out of place: uout = GS^k(u_in)
+// where u_in = 0 (mode 1), uin (mode 0) or uin + P(uc) (mode 2: prolongation
+// of the coarse level uc (coarse n = n/2, pitch pitchc) added on load).
+constexpr int kSmoothMaxSweeps = 3;
+void launch_smooth(const double *uin, double *uout, const double *rhs, const double *v1,
+                   const double *v2, const double *uc, long pitchc, long n, long pitch, Coef c,
+                   int sweeps, int mode, hipStream_t s);
 // One colour, in place (two launches make a sweep).  Reference for A/B timing.
 void launch_gs_colour(double *u, const double *rhs, const double *v1, const double *v2,
                       long n, long pitch, Coef c, int colour, hipStream_t s);

@@ -359,6 +359,171 @@ __global__ __launch_bounds__(BLOCK) void k_gs_sweep(const double *__restrict__ u
 #undef MGX_GS_STEP
 }
 
+// k_smooth: K red-black sweeps in ONE pass over HBM (temporal blocking).
+//
+// The 2K half-sweeps are "stages" h = 0..S-1 (S = 2K; even h red, odd h
+// black).  A workgroup marches down the rows of a strip; at step s stage h
+// updates its colour in row s+1-h, reading the other colour of rows
+// s-h..s+2-h as left by stage h-1.  One barrier separates consecutive stages.
+// u rows live in an LDS ring of S+3 rows; each lane owns one column pair.
+//
+// Halo: the outer H = K lanes on each side own halo pairs that are loaded and
+// updated like the strip but never stored.  Stage h is exact on a region that
+// shrinks by one column (and one row) per stage, so after S stages the strip
+// [j0, j0+W) and the rows [a, b) are exact; values outside that cone may be
+// garbage and are never stored or read by exact values.  Every exact value is
+// computed from exactly the operands the sequential gs.cpp:109-189 sweeps
+// use, so the result is bitwise that of K reference sweeps.
+//
+// rhs / v1 / v2 of a row stay in registers from the step they are loaded
+// until the last stage that needs them (S+1 rows); the register ring is
+// statically indexed by unrolling the step loop by NS = S+1.
+//
+// MODE bit 1 (ZERO): u_in is identically zero (u[l+1]=0, multigrid.cpp:77),
+// no u loads.  MODE bit 2 (PROLONG): every loaded u value first gets the
+// bilinear prolongation of the coarse correction added (u += P(uc),
+// multigrid.cpp:81-83, gs.cpp:238-265 expressions), i.e. prolong+add+smooth
+// in one pass.
+//
+// Work split: a 1-D grid of G workgroups, each gets an equal share of the
+// strip-major (strip, row) space, so one launch is one balanced wave.
+struct RowData {
+    double2 r, x, y;
+};
+
+template <int BLOCK, int K, int MODE>
+__global__ __launch_bounds__(BLOCK) void k_smooth(
+    const double *__restrict__ uin, double *__restrict__ uout, const double *__restrict__ rhs,
+    const double *__restrict__ v1, const double *__restrict__ v2, const double *__restrict__ uc,
+    long pitchc, int n, long pitch, int strips, long units_per_wg, Coef c) {
+    constexpr int S = 2 * K;          // stages
+    constexpr int H = K;              // halo pairs per side (2H >= S columns)
+    constexpr int NR = S + 3;         // LDS ring rows
+    constexpr int NS = S + 1;         // register ring rows (= unroll period)
+    constexpr int LW = 2 * BLOCK + 2; // LDS row: x = 1 + 2*lane + cs
+    constexpr int W = 2 * (BLOCK - 2 * H);
+    constexpr bool ZERO = (MODE & 1) != 0;
+    constexpr bool PROL = (MODE & 2) != 0;
+    __shared__ __attribute__((aligned(16))) double ring[NR][LW];
+
+    const int l = threadIdx.x;
+    const long total = (long)strips * (n + 1);
+    long start = (long)blockIdx.x * units_per_wg;
+    const long end = min(total, start + units_per_wg);
+    const int nc = n >> 1;
+
+    auto slot = [](long r) -> int { return (int)(((r % NR) + NR) % NR); };
+
+    while (start < end) {
+        const int strip = (int)(start / (n + 1));
+        const int a = (int)(start % (n + 1));
+        const int b = (int)min((long)(n + 1), (long)a + (end - start));
+        start += b - a;
+
+        const long j0 = (long)strip * W;
+        const long c0 = j0 - 2 * H + 2 * l;
+        const bool act = c0 >= 0 && c0 <= n;
+        const bool keep = act && l >= H && l < BLOCK - H;
+
+        // prefetched u row (+ coarse operands of its prolongation)
+        double2 X = make_double2(0.0, 0.0);
+        double q00 = 0.0, q01 = 0.0, q10 = 0.0, q11 = 0.0;
+        long xrow = 0;
+        auto load_u = [&](long R) {
+            xrow = R;
+            if (ZERO || !act || R < 0 || R > n) return;
+            X = ld2(uin + R * pitch + c0);
+            if (PROL) {
+                const long i = R >> 1, j = c0 >> 1;
+                const double *p0 = uc + i * pitchc + j;
+                q00 = p0[0];
+                q01 = (j + 1 <= nc) ? p0[1] : 0.0;
+                if (R & 1) {
+                    q10 = p0[pitchc];
+                    q11 = (j + 1 <= nc) ? p0[pitchc + 1] : 0.0;
+                }
+            }
+        };
+        auto put_u = [&]() {
+            const long R = xrow;
+            double2 v = X;
+            if (ZERO) v = make_double2(0.0, 0.0);
+            if (PROL && act && R >= 0 && R <= n) {
+                double2 pr;
+                if (!(R & 1)) {
+                    pr.x = q00;
+                    pr.y = (q00 + q01) / 2;
+                } else {
+                    pr.x = (q00 + q10) / 2;
+                    pr.y = (q00 + q10 + q01 + q11) / 4;
+                }
+                v.x = v.x + pr.x;
+                v.y = v.y + pr.y;
+            }
+            st2(&ring[slot(R)][1 + 2 * l], v);
+        };
+        auto load_rv = [&](long R, RowData &d) {
+            if (!act || R < 0 || R > n) return;
+            const long o = R * pitch + c0;
+            d.r = ld2(rhs + o);
+            d.x = ld2(v1 + o);
+            d.y = ld2(v2 + o);
+        };
+        auto stage = [&](int h, long r, const RowData &d) {
+            if (!act || r < 1 || r > n - 1) return;
+            const int cs = (int)(r & 1) ^ (h & 1);
+            const long col = c0 + cs;
+            if (col < 1 || col > n - 1) return;
+            const int x = 1 + 2 * l + cs;
+            double *row = ring[slot(r)];
+            const double uN = ring[slot(r - 1)][x], uS = ring[slot(r + 1)][x];
+            row[x] = gs_point(sel(d.r, cs), sel(d.x, cs), sel(d.y, cs), uN, row[x - 1], uS,
+                              row[x + 1], c);
+        };
+
+        const long s_first = (long)a - S;
+        const long s_last = (long)b + S - 3;
+        // align the first step to the register-ring period (extra leading steps
+        // only compute values outside the exact cone)
+        long s = s_first >= 0 ? (s_first / NS) * NS : -(((-s_first) + NS - 1) / NS) * NS;
+
+        RowData rd[NS];
+#pragma unroll
+        for (int q = 0; q < NS; ++q) rd[q].r = rd[q].x = rd[q].y = make_double2(0.0, 0.0);
+        // prologue: LDS rows s..s+2, X = u row s+3, rd[1] = rhs/v row s+1
+        for (int d = 0; d < 3; ++d) {
+            load_u(s + d);
+            put_u();
+        }
+        load_u(s + 3);
+        load_rv(s + 1, rd[1]);
+        __syncthreads();
+
+        for (;;) {
+#pragma unroll
+            for (int p = 0; p < NS; ++p) {
+                // (1) u row s+3 into the ring, prefetch u row s+4 and rhs/v row s+2
+                put_u();
+                load_u(s + 4);
+                load_rv(s + 2, rd[(p + 2) % NS]);
+                // (2) the S stages
+#pragma unroll
+                for (int h = 0; h < S; ++h) {
+                    stage(h, s + 1 - h, rd[(p + 1 - h + 2 * NS) % NS]);
+                    __syncthreads();
+                }
+                // (3) output row s+2-S is final
+                const long ro = s + 2 - S;
+                if (keep && ro >= a && ro < b)
+                    st2(uout + ro * pitch + c0, ld2(&ring[slot(ro)][1 + 2 * l]));
+                if (++s > s_last) goto done;
+            }
+        }
+    done:
+        __syncthreads();
+    }
+}
+
 // One colour in place (two launches = one sweep).  Grid (strips, interior rows).
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void k_gs_colour(double *u, const double *rhs,
@@ -635,6 +800,61 @@ void launch_gs_sweep(const double *uin, double *uout, const double *rhs, const d
         else
             MGX_LAUNCH((k_gs_sweep<B, false>), g, dim3(B), s, uin, uout, rhs, v1, v2, (int)n,
                        pitch, R, c);
+    }
+}
+
+template <int BLOCK, int K, int MODE>
+static void smooth_inst(const double *uin, double *uout, const double *rhs, const double *v1,
+                        const double *v2, const double *uc, long pitchc, long n, long pitch,
+                        Coef c, hipStream_t s) {
+    constexpr int W = 2 * (BLOCK - 2 * K);
+    static int slots = 0;   // resident workgroups of this instantiation
+    if (!slots) {
+        int dev = 0, cus = 0, per = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_smooth<BLOCK, K, MODE>,
+                                                           BLOCK, 0);
+        slots = std::max(1, cus) * std::max(1, per);
+    }
+    const int strips = (int)((n + 1 + W - 1) / W);
+    const long total = (long)strips * (n + 1);
+    // at least ~64 rows per workgroup so the 2S-row priming stays cheap
+    const long g = std::max<long>(1, std::min<long>(slots, total / 64));
+    const long upw = (total + g - 1) / g;
+    const unsigned grid = (unsigned)((total + upw - 1) / upw);
+    MGX_LAUNCH((k_smooth<BLOCK, K, MODE>), dim3(grid), dim3(BLOCK), s, uin, uout, rhs, v1, v2,
+               uc, pitchc, (int)n, pitch, strips, upw, c);
+}
+
+template <int K, int MODE>
+static void smooth_block(const double *uin, double *uout, const double *rhs, const double *v1,
+                         const double *v2, const double *uc, long pitchc, long n, long pitch,
+                         Coef c, hipStream_t s) {
+    if (n >= 4096)
+        smooth_inst<256, K, MODE>(uin, uout, rhs, v1, v2, uc, pitchc, n, pitch, c, s);
+    else
+        smooth_inst<64, K, MODE>(uin, uout, rhs, v1, v2, uc, pitchc, n, pitch, c, s);
+}
+
+template <int K>
+static void smooth_k(const double *uin, double *uout, const double *rhs, const double *v1,
+                     const double *v2, const double *uc, long pitchc, long n, long pitch,
+                     Coef c, int mode, hipStream_t s) {
+    switch (mode) {
+        case 1: smooth_block<K, 1>(uin, uout, rhs, v1, v2, uc, pitchc, n, pitch, c, s); break;
+        case 2: smooth_block<K, 2>(uin, uout, rhs, v1, v2, uc, pitchc, n, pitch, c, s); break;
+        default: smooth_block<K, 0>(uin, uout, rhs, v1, v2, uc, pitchc, n, pitch, c, s); break;
+    }
+}
+
+void launch_smooth(const double *uin, double *uout, const double *rhs, const double *v1,
+                   const double *v2, const double *uc, long pitchc, long n, long pitch, Coef c,
+                   int sweeps, int mode, hipStream_t s) {
+    switch (sweeps) {
+        case 1: smooth_k<1>(uin, uout, rhs, v1, v2, uc, pitchc, n, pitch, c, mode, s); break;
+        case 2: smooth_k<2>(uin, uout, rhs, v1, v2, uc, pitchc, n, pitch, c, mode, s); break;
+        default: smooth_k<3>(uin, uout, rhs, v1, v2, uc, pitchc, n, pitch, c, mode, s); break;
     }
 }
 

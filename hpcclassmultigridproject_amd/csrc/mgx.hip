@@ -9,6 +9,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -142,11 +143,39 @@ int materialize(mgx_ctx *c, int l) {
     return MGX_OK;
 }
 
-// `sweeps` RB-GS sweeps (gauss_seidel, gs.cpp:109).
-int op_gs(mgx_ctx *c, int l, int sweeps) {
+// `sweeps` RB-GS sweeps (gauss_seidel, gs.cpp:109).  With prolong = true the
+// coarse correction u[l] += P(u[l+1]) (multigrid.cpp:81-83) is applied first,
+// fused into the first smoothing pass when the smoother supports it.
+int op_prolong_add(mgx_ctx *c, int l);
+int op_gs(mgx_ctx *c, int l, int sweeps, bool prolong = false) {
     Level &L = c->lv[l];
+    if (c->opt.smoother == 0) {
+        int done = 0;
+        while (done < sweeps || (prolong && sweeps == 0)) {
+            const int k = std::min(sweeps - done, std::max(1, std::min(c->opt.fuse, mgx::kSmoothMaxSweeps)));
+            if (k <= 0) break;
+            const bool z = L.zero;
+            const bool pr = prolong && done == 0;
+            if (pr) CHK(materialize(c, l + 1));
+            const int mode = z ? 1 : (pr ? 2 : 0);
+            const Level *C = pr ? &c->lv[l + 1] : nullptr;
+            double bytes = 40.0 * k * L.M();
+            if (pr) bytes += 32.0 * L.M() + 8.0 * C->M();
+            CHK(launch(c, pr ? MGX_K_PSMOOTH : MGX_K_GS, l, bytes, [&] {
+                mgx::launch_smooth(L.u[L.cur], L.u[L.cur ^ 1], L.rhs, L.v1, L.v2,
+                                   C ? C->U() : nullptr, C ? C->pitch : 0, L.n, L.pitch, L.coef,
+                                   k, mode, c->stream);
+            }));
+            L.cur ^= 1;
+            L.zero = false;
+            done += k;
+        }
+        if (prolong && sweeps == 0) CHK(op_prolong_add(c, l));
+        return MGX_OK;
+    }
+    if (prolong) CHK(op_prolong_add(c, l));
     for (int k = 0; k < sweeps; ++k) {
-        if (c->opt.smoother == 0) {
+        if (c->opt.smoother == 2) {
             const bool z = L.zero;
             CHK(launch(c, MGX_K_GS, l, 40.0 * L.M(), [&] {
                 mgx::launch_gs_sweep(L.u[L.cur], L.u[L.cur ^ 1], L.rhs, L.v1, L.v2, L.n, L.pitch,
@@ -238,8 +267,7 @@ int op_vcycle(mgx_ctx *c, int l) {
             CHK(op_gs(c, l, c->opt.nsmooth));
             CHK(op_restrict(c, l));
             CHK(op_vcycle(c, l + 1));
-            CHK(op_prolong_add(c, l));
-            CHK(op_gs(c, l, c->opt.nsmooth));
+            CHK(op_gs(c, l, c->opt.nsmooth, /*prolong=*/true));
         }
     }
     return MGX_OK;
@@ -370,6 +398,7 @@ void mgx_default_options(mgx_options *o) {
     o->coarse_maxit = 1000;  // multigrid.cpp:60
     o->max_cycle = 50;       // multigrid.cpp:94
     o->smoother = 0;
+    o->fuse = 3;
 }
 
 // ---- gs.h mirror (reference layout, device pointers, null stream)
@@ -425,7 +454,9 @@ int mgx_create(mgx_ctx **out, long n, int maxlvl, double dt, double nu, const mg
     mgx_options o;
     mgx_default_options(&o);
     if (opt) o = *opt;
-    if (o.nsmooth < 0 || o.shape < 1 || o.coarse_maxit < 1 || o.max_cycle < 1)
+    if (o.fuse < 1 || o.fuse > mgx::kSmoothMaxSweeps) o.fuse = mgx::kSmoothMaxSweeps;
+    if (o.nsmooth < 0 || o.shape < 1 || o.coarse_maxit < 1 || o.max_cycle < 1 ||
+        o.smoother < 0 || o.smoother > 2)
         return fail(MGX_E_ARG, "mgx_create: bad options");
     mgx_ctx *c = new mgx_ctx();
     c->N = n;

@@ -54,11 +54,12 @@ class Multigrid:
     """Device-resident level towers and the V-cycle (mgx_ctx)."""
 
     def __init__(self, N, maxlvl, dt, nu, *, nsmooth=3, shape=1,
-                 tower_mode=_lib.TOWER_REFERENCE, device=-1, smoother=0, coarse_tol=1e-5,
-                 coarse_maxit=1000, max_cycle=50):
+                 tower_mode=_lib.TOWER_REFERENCE, device=-1, smoother=0, fuse=3,
+                 coarse_tol=1e-5, coarse_maxit=1000, max_cycle=50):
         self.N, self.maxlvl, self.dt, self.nu = N, maxlvl, dt, nu
         self.opt = default_options(nsmooth=nsmooth, shape=shape, tower_mode=tower_mode,
-                                   device=device, smoother=smoother, coarse_tol=coarse_tol,
+                                   device=device, smoother=smoother, fuse=fuse,
+                                   coarse_tol=coarse_tol,
                                    coarse_maxit=coarse_maxit, max_cycle=max_cycle)
         h = C.c_void_p()
         check(lib().mgx_create(C.byref(h), N, maxlvl, dt, nu, C.byref(self.opt)))

@@ -81,7 +81,11 @@ typedef struct mgx_options {
     double coarse_tol;  /* coarsest-level GS stop, absolute (multigrid.cpp:60: 1e-5) */
     int coarse_maxit;   /* coarsest-level GS cap (multigrid.cpp:60: 1000) */
     int max_cycle;      /* mg_outer cycle cap (multigrid.cpp:94: 50) */
-    int smoother;       /* 0 = fused one-pass RB sweep (default), 1 = two colour passes */
+    int smoother;       /* 0 = temporally blocked passes of up to `fuse` sweeps with
+                           the prolongation fused into the post-smoothing pass
+                           (default); 1 = two in-place colour passes per sweep;
+                           2 = one-pass single sweeps (no temporal blocking) */
+    int fuse;           /* smoother 0: max RB sweeps per HBM pass, 1..3 (default 3) */
 } mgx_options;
 
 /* Fills *opt with the reference defaults. */
@@ -157,7 +161,8 @@ int mgx_synchronize(mgx_ctx *ctx);
 #define MGX_K_COARSE 4         /* coarsest-level solve */
 #define MGX_K_RHS 5            /* compute_rhs */
 #define MGX_K_HALO 6           /* halo exchange (multi-GPU) */
-#define MGX_K_COUNT 7
+#define MGX_K_PSMOOTH 7        /* prolongation + add fused into a smoothing pass */
+#define MGX_K_COUNT 8
 int mgx_profile_enable(mgx_ctx *ctx, int on);
 int mgx_profile_reset(mgx_ctx *ctx);
 /* For kernel kind `kind` on level `level` (-1 = all levels): launches, summed

@@ -14,7 +14,9 @@ from conftest import load_golden
 from hpcclassmultigridproject_amd import Multigrid, gs, init_problem
 
 pytestmark = pytest.mark.gpu
-NORM_RTOL = 1e-13
+# Serial (reference) vs tree summation of M positive squares: relative error
+# bound ~M*eps; measured 1.3e-13 at M=1e6.  Tolerance for norms:
+NORM_RTOL = 1e-11
 DEV = "cuda:0"
 
 
@@ -96,14 +98,18 @@ def test_context_tower_matches_oracle(oracle_mod, tower_mode):
                 assert np.array_equal(mg.download_level(l, f), t.level(f, l)[: (n + 1) ** 2]), (l, f)
 
 
-@pytest.mark.parametrize("smoother", [0, 1])
-@pytest.mark.parametrize("N", [16, 128, 512, 4096])
-def test_context_gs_bitwise_vs_oracle(oracle_mod, N, smoother):
-    """One-pass fused RB sweep (0) and two-colour passes (1) == gs.cpp:109."""
+SMOOTHERS = [(0, 3), (0, 2), (0, 1), (1, 3), (2, 3)]   # (smoother, sweeps fused per pass)
+
+
+@pytest.mark.parametrize("smoother,fuse", SMOOTHERS)
+@pytest.mark.parametrize("N", [16, 128, 512, 4096, 8192])
+def test_context_gs_bitwise_vs_oracle(oracle_mod, N, smoother, fuse):
+    """Temporally blocked passes (0), two-colour passes (1) and one-pass single
+    sweeps (2) all equal 3 x gs.cpp:109 bitwise."""
     O = oracle_mod
     u0, v1, v2 = init_problem(N)
     dt, nu = 1.0 / N / 10, -4e-4
-    with Multigrid(N, 1, dt, nu, smoother=smoother) as mg:
+    with Multigrid(N, 1, dt, nu, smoother=smoother, fuse=fuse) as mg:
         mg.upload(u0, v1, v2)
         mg.rhs()
         rhs = O.compute_rhs(u0, N, v1, v2, dt, nu, 1.0 / N)
