@@ -15,7 +15,7 @@ namespace mgx {
 // reference's own expressions: rr = 0.5*k/(h*h) (gs.cpp:9-11),
 // dgs = 1.0-4.0*rr*nu (gs.cpp:130, :75), drhs = 1.0+4.0*rr*nu (gs.cpp:44).
 struct Coef {
-    double rr, nu, h, dgs, drhs;
+    double rr, nu, h, dgs, drhs, rdgs;   // rdgs = RN(1/dgs)
 };
 Coef make_coef(double k, double nu, double h);
 
@@ -47,12 +47,27 @@ void launch_gs_sweep(const double *uin, double *uout, const double *rhs, const d
                      const double *v2, long n, long pitch, Coef c, bool zero_in,
                      hipStream_t s);
 // `sweeps` (1..3) red-black sweeps in one pass, out of place: uout = GS^k(u_in)
-// where u_in = 0 (mode 1), uin (mode 0) or uin + P(uc) (mode 2: prolongation
+// where u_in = 0 (mode bit 1), uin, or uin + P(uc) (mode bit 2: prolongation
 // of the coarse level uc (coarse n = n/2, pitch pitchc) added on load).
+// Mode bit 4: the residual of uout at the even-even points is written to the
+// coarse rhs rhsc (pitchc); mode bit 8: the residual norm of uout is written
+// to *norm_out (partials: norm_partials_size() doubles).  Returns the number
+// of workgroups launched, -1 for an unsupported (sweeps, mode).
 constexpr int kSmoothMaxSweeps = 3;
-void launch_smooth(const double *uin, double *uout, const double *rhs, const double *v1,
-                   const double *v2, const double *uc, long pitchc, long n, long pitch, Coef c,
-                   int sweeps, int mode, hipStream_t s);
+enum : int { kModeZero = 1, kModeProlong = 2, kModeRestrict = 4, kModeNorm = 8 };
+struct SmoothArgs {
+    const double *uin;
+    double *uout;
+    const double *rhs, *v1, *v2;
+    long n, pitch;
+    Coef c;
+    const double *uc;   // coarse u (PROLONG)
+    double *rhsc;       // coarse rhs (RESTRICT)
+    long pitchc;        // pitch of the coarse level
+    double *partials;   // NORM
+    double *norm_out;   // NORM
+};
+int launch_smooth(const SmoothArgs &a, int sweeps, int mode, hipStream_t s);
 // One colour, in place (two launches make a sweep).  Reference for A/B timing.
 void launch_gs_colour(double *u, const double *rhs, const double *v1, const double *v2,
                       long n, long pitch, Coef c, int colour, hipStream_t s);

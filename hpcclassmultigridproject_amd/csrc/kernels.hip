@@ -20,6 +20,7 @@ Coef make_coef(double k, double nu, double h) {
     c.h = h;
     c.dgs = 1.0 - 4.0 * c.rr * nu;       // gs.cpp:130 denominator, gs.cpp:75 diagonal
     c.drhs = 1.0 + 4.0 * c.rr * nu;      // gs.cpp:44
+    c.rdgs = 1.0 / c.dgs;                // RN(1/d) for the Markstein division
     return c;
 }
 
@@ -365,25 +366,37 @@ __global__ __launch_bounds__(BLOCK) void k_gs_sweep(const double *__restrict__ u
 // black).  A workgroup marches down the rows of a strip; at step s stage h
 // updates its colour in row s+1-h, reading the other colour of rows
 // s-h..s+2-h as left by stage h-1.  One barrier separates consecutive stages.
-// u rows live in an LDS ring of S+3 rows; each lane owns one column pair.
+// u rows live in an LDS ring; each lane owns one column pair (2c, 2c+1).
+// Optional last stage h = S (RESTRICT / NORM): the residual of row s+1-S,
+// whose neighbours are final by then.
 //
-// Halo: the outer H = K lanes on each side own halo pairs that are loaded and
+// Halo: the outer H lanes on each side own halo pairs that are loaded and
 // updated like the strip but never stored.  Stage h is exact on a region that
-// shrinks by one column (and one row) per stage, so after S stages the strip
-// [j0, j0+W) and the rows [a, b) are exact; values outside that cone may be
-// garbage and are never stored or read by exact values.  Every exact value is
-// computed from exactly the operands the sequential gs.cpp:109-189 sweeps
-// use, so the result is bitwise that of K reference sweeps.
+// shrinks by one column (and one row) per stage, so after E stages (E = S,
+// +1 with a residual stage, H = ceil(E/2)) the strip [j0, j0+W) and the rows
+// [a, b) are exact; values outside that cone may be garbage and are never
+// stored or read by exact values.  Every exact value is computed from exactly
+// the operands the sequential gs.cpp:109-189 sweeps use, so the result is
+// bitwise that of K reference sweeps.
 //
-// rhs / v1 / v2 of a row stay in registers from the step they are loaded
-// until the last stage that needs them (S+1 rows); the register ring is
-// statically indexed by unrolling the step loop by NS = S+1.
+// rhs / v1 / v2 of a row stay in registers from the step they are loaded to
+// the last stage that needs them.  The step loop is unrolled by NS = S+2
+// (even), and its start aligned to NS, so every register-ring index and the
+// parity of every row are compile-time constants: no selects, static LDS
+// offsets.  Ring slots are scalar (SALU) arithmetic.
 //
-// MODE bit 1 (ZERO): u_in is identically zero (u[l+1]=0, multigrid.cpp:77),
-// no u loads.  MODE bit 2 (PROLONG): every loaded u value first gets the
-// bilinear prolongation of the coarse correction added (u += P(uc),
-// multigrid.cpp:81-83, gs.cpp:238-265 expressions), i.e. prolong+add+smooth
-// in one pass.
+// Division by the diagonal 1-4*rr*nu uses the host-computed y = RN(1/d) and
+// one Markstein correction: q0 = a*y, r = fma(-q0,d,a), q = fma(r,y,q0)
+// (q0 if r == 0, which keeps the sign of a zero).  With y = RN(1/d) this is
+// the correctly rounded quotient (Markstein's theorem), i.e. bitwise a/d;
+// tools/check_division.c tests it on 1.4e9 random operands.
+//
+// MODE bits: 1 ZERO (u_in == 0, multigrid.cpp:77: no u loads); 2 PROLONG
+// (u_in = uin + P(uc): the bilinear prolongation of the coarse correction,
+// gs.cpp:238-265 expressions, added on load = multigrid.cpp:81-83 fused);
+// 4 RESTRICT (residual at the fine even-even points written to the coarse
+// rhs, multigrid.cpp:73-75 fused); 8 NORM (sum of squared residuals of the
+// interior: per-workgroup partials, multigrid.cpp:112-113 fused).
 //
 // Work split: a 1-D grid of G workgroups, each gets an equal share of the
 // strip-major (strip, row) space, so one launch is one balanced wave.
@@ -391,19 +404,43 @@ struct RowData {
     double2 r, x, y;
 };
 
+__device__ __forceinline__ double div_diag(double a, const Coef &c) {
+    const double q0 = a * c.rdgs;
+    const double r = __builtin_fma(-q0, c.dgs, a);
+    return r == 0.0 ? q0 : __builtin_fma(r, c.rdgs, q0);
+}
+// gs.cpp:130 with the Markstein division (bitwise equal to gs_point).
+__device__ __forceinline__ double gs_point_fast(double rhs, double v1, double v2, double uN,
+                                                double uW, double uS, double uE,
+                                                const Coef &c) {
+    const double aa = coef_a(v2, c), bb = coef_b(v2, c);
+    const double cc = coef_a(v1, c), dd = coef_b(v1, c);
+    return div_diag(rhs - cc * uN - aa * uW - dd * uS - bb * uE, c);
+}
+
+template <int K, int MODE>
+struct SmoothCfg {
+    static constexpr bool ZERO = (MODE & 1) != 0;
+    static constexpr bool PROL = (MODE & 2) != 0;
+    static constexpr bool REST = (MODE & 4) != 0;
+    static constexpr bool NORM = (MODE & 8) != 0;
+    static constexpr int S = 2 * K;                      // smoothing stages
+    static constexpr int E = S + ((REST || NORM) ? 1 : 0);  // + residual stage
+    static constexpr int H = (E + 1) / 2;                // halo pairs per side
+    static constexpr int NR = E + 3;                     // LDS ring rows
+    static constexpr int NS = S + 2;                     // register ring rows / unroll
+};
+
 template <int BLOCK, int K, int MODE>
 __global__ __launch_bounds__(BLOCK) void k_smooth(
     const double *__restrict__ uin, double *__restrict__ uout, const double *__restrict__ rhs,
     const double *__restrict__ v1, const double *__restrict__ v2, const double *__restrict__ uc,
-    long pitchc, int n, long pitch, int strips, long units_per_wg, Coef c) {
-    constexpr int S = 2 * K;          // stages
-    constexpr int H = K;              // halo pairs per side (2H >= S columns)
-    constexpr int NR = S + 3;         // LDS ring rows
-    constexpr int NS = S + 1;         // register ring rows (= unroll period)
-    constexpr int LW = 2 * BLOCK + 2; // LDS row: x = 1 + 2*lane + cs
+    long pitchc, double *__restrict__ rhsc, double *__restrict__ partials, int n, long pitch,
+    int strips, long units_per_wg, Coef c) {
+    using C = SmoothCfg<K, MODE>;
+    constexpr int S = C::S, E = C::E, H = C::H, NR = C::NR, NS = C::NS;
+    constexpr int LW = 2 * BLOCK + 2;   // LDS row: x = 1 + 2*lane + cs
     constexpr int W = 2 * (BLOCK - 2 * H);
-    constexpr bool ZERO = (MODE & 1) != 0;
-    constexpr bool PROL = (MODE & 2) != 0;
     __shared__ __attribute__((aligned(16))) double ring[NR][LW];
 
     const int l = threadIdx.x;
@@ -411,8 +448,7 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
     long start = (long)blockIdx.x * units_per_wg;
     const long end = min(total, start + units_per_wg);
     const int nc = n >> 1;
-
-    auto slot = [](long r) -> int { return (int)(((r % NR) + NR) % NR); };
+    double acc = 0.0;   // NORM partial
 
     while (start < end) {
         const int strip = (int)(start / (n + 1));
@@ -424,16 +460,20 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
         const long c0 = j0 - 2 * H + 2 * l;
         const bool act = c0 >= 0 && c0 <= n;
         const bool keep = act && l >= H && l < BLOCK - H;
+        // per-lane interior flags of the two columns of the pair
+        const bool in0 = act && c0 >= 1 && c0 <= n - 1;
+        const bool in1 = act && c0 + 1 <= n - 1;
+        const int x0 = 1 + 2 * l;
 
         // prefetched u row (+ coarse operands of its prolongation)
         double2 X = make_double2(0.0, 0.0);
         double q00 = 0.0, q01 = 0.0, q10 = 0.0, q11 = 0.0;
-        long xrow = 0;
-        auto load_u = [&](long R) {
+        int xrow = 0;
+        auto load_u = [&](int R) {
             xrow = R;
-            if (ZERO || !act || R < 0 || R > n) return;
-            X = ld2(uin + R * pitch + c0);
-            if (PROL) {
+            if (C::ZERO || !act || R < 0 || R > n) return;
+            X = ld2(uin + (long)R * pitch + c0);
+            if (C::PROL) {
                 const long i = R >> 1, j = c0 >> 1;
                 const double *p0 = uc + i * pitchc + j;
                 q00 = p0[0];
@@ -444,11 +484,11 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
                 }
             }
         };
-        auto put_u = [&]() {
-            const long R = xrow;
+        auto put_u = [&](int sl) {
+            const int R = xrow;
             double2 v = X;
-            if (ZERO) v = make_double2(0.0, 0.0);
-            if (PROL && act && R >= 0 && R <= n) {
+            if (C::ZERO) v = make_double2(0.0, 0.0);
+            if (C::PROL && act && R >= 0 && R <= n) {
                 double2 pr;
                 if (!(R & 1)) {
                     pr.x = q00;
@@ -460,40 +500,36 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
                 v.x = v.x + pr.x;
                 v.y = v.y + pr.y;
             }
-            st2(&ring[slot(R)][1 + 2 * l], v);
+            st2(&ring[sl][x0], v);
         };
-        auto load_rv = [&](long R, RowData &d) {
+        auto load_rv = [&](int R, RowData &d) {
             if (!act || R < 0 || R > n) return;
-            const long o = R * pitch + c0;
+            const long o = (long)R * pitch + c0;
             d.r = ld2(rhs + o);
             d.x = ld2(v1 + o);
             d.y = ld2(v2 + o);
         };
-        auto stage = [&](int h, long r, const RowData &d) {
-            if (!act || r < 1 || r > n - 1) return;
-            const int cs = (int)(r & 1) ^ (h & 1);
-            const long col = c0 + cs;
-            if (col < 1 || col > n - 1) return;
-            const int x = 1 + 2 * l + cs;
-            double *row = ring[slot(r)];
-            const double uN = ring[slot(r - 1)][x], uS = ring[slot(r + 1)][x];
-            row[x] = gs_point(sel(d.r, cs), sel(d.x, cs), sel(d.y, cs), uN, row[x - 1], uS,
-                              row[x + 1], c);
-        };
 
-        const long s_first = (long)a - S;
-        const long s_last = (long)b + S - 3;
-        // align the first step to the register-ring period (extra leading steps
-        // only compute values outside the exact cone)
-        long s = s_first >= 0 ? (s_first / NS) * NS : -(((-s_first) + NS - 1) / NS) * NS;
+        const int s_first = a - E;
+        const int s_last = b + E - 3;
+        // align the first step to the unroll period NS (even): then the parity
+        // of s equals the parity of the unrolled copy index.  Leading extra
+        // steps only compute values outside the exact cone.
+        int s = s_first >= 0 ? (s_first / NS) * NS : -(((-s_first) + NS - 1) / NS) * NS;
+        s = __builtin_amdgcn_readfirstlane(s);
+        // ring slot of row s: base = s mod NR (scalar)
+        int base = ((s % NR) + NR) % NR;
 
         RowData rd[NS];
 #pragma unroll
         for (int q = 0; q < NS; ++q) rd[q].r = rd[q].x = rd[q].y = make_double2(0.0, 0.0);
-        // prologue: LDS rows s..s+2, X = u row s+3, rd[1] = rhs/v row s+1
+        // prologue: ring rows s..s+2, X = u row s+3, rd[1] = rhs/v row s+1
+#pragma unroll
         for (int d = 0; d < 3; ++d) {
             load_u(s + d);
-            put_u();
+            int sl = base + d;
+            sl -= sl >= NR ? NR : 0;
+            put_u(sl);
         }
         load_u(s + 3);
         load_rv(s + 1, rd[1]);
@@ -502,25 +538,84 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
         for (;;) {
 #pragma unroll
             for (int p = 0; p < NS; ++p) {
+                // slot(s + d) for d in [-E, 3], scalar
+                auto slot = [&](int d) {
+                    int t = base + d;
+                    if (d > 0) t -= t >= NR ? NR : 0;
+                    if (d < 0) t += t < 0 ? NR : 0;
+                    return t;
+                };
                 // (1) u row s+3 into the ring, prefetch u row s+4 and rhs/v row s+2
-                put_u();
+                put_u(slot(3));
                 load_u(s + 4);
                 load_rv(s + 2, rd[(p + 2) % NS]);
-                // (2) the S stages
+                // (2) the S smoothing stages
 #pragma unroll
                 for (int h = 0; h < S; ++h) {
-                    stage(h, s + 1 - h, rd[(p + 1 - h + 2 * NS) % NS]);
+                    const int r = s + 1 - h;
+                    // parity of r is static: s == p (mod 2)
+                    const int cs = ((p + 1 - h) & 1) ^ (h & 1);
+                    const bool inr = r >= 1 && r <= n - 1;
+                    if (inr && (cs ? in1 : in0)) {
+                        const RowData &d = rd[(p + 1 - h + 2 * NS) % NS];
+                        double *row = ring[slot(1 - h)];
+                        const int x = x0 + cs;
+                        const double uN = ring[slot(-h)][x], uS = ring[slot(2 - h)][x];
+                        row[x] = gs_point_fast(cs ? d.r.y : d.r.x, cs ? d.x.y : d.x.x,
+                                               cs ? d.y.y : d.y.x, uN, row[x - 1], uS,
+                                               row[x + 1], c);
+                    }
                     __syncthreads();
                 }
                 // (3) output row s+2-S is final
-                const long ro = s + 2 - S;
-                if (keep && ro >= a && ro < b)
-                    st2(uout + ro * pitch + c0, ld2(&ring[slot(ro)][1 + 2 * l]));
+                {
+                    const int ro = s + 2 - S;
+                    if (keep && ro >= a && ro < b)
+                        st2(uout + (long)ro * pitch + c0, ld2(&ring[slot(2 - S)][x0]));
+                }
+                // (4) residual stage on row s+1-S
+                if (C::REST || C::NORM) {
+                    const int r = s + 1 - S;
+                    const RowData &d = rd[(p + 1 - S + 2 * NS) % NS];
+                    if (keep && r >= a && r < b && r >= 1 && r <= n - 1) {
+                        const double *rm = ring[slot(1 - S)], *rn_ = ring[slot(-S)],
+                                     *rs_ = ring[slot(2 - S)];
+                        if (C::REST) {
+                            // even-even points only: r even (static), c0 = 2J
+                            if (((p + 1 - S) & 1) == 0 && in0 && c0 <= n - 2 && r <= n - 2) {
+                                const double res =
+                                    res_point(d.r.x, d.x.x, d.y.x, rm[x0], rn_[x0], rm[x0 - 1],
+                                              rs_[x0], rm[x0 + 1], c);
+                                rhsc[(long)(r >> 1) * pitchc + (c0 >> 1)] = res;
+                            }
+                        } else {
+                            if (in0) {
+                                const double res =
+                                    res_point(d.r.x, d.x.x, d.y.x, rm[x0], rn_[x0], rm[x0 - 1],
+                                              rs_[x0], rm[x0 + 1], c);
+                                acc += res * res;
+                            }
+                            if (in1) {
+                                const double res =
+                                    res_point(d.r.y, d.x.y, d.y.y, rm[x0 + 1], rn_[x0 + 1],
+                                              rm[x0], rs_[x0 + 1], rm[x0 + 2], c);
+                                acc += res * res;
+                            }
+                        }
+                    }
+                }
+                ++base;
+                base -= base >= NR ? NR : 0;
                 if (++s > s_last) goto done;
             }
         }
     done:
         __syncthreads();
+    }
+    if (C::NORM) {
+        __shared__ double red_lds[BLOCK / 64];
+        const double tot = block_sum(acc, red_lds);
+        if (l == 0) partials[blockIdx.x] = tot;
     }
 }
 
@@ -804,10 +899,8 @@ void launch_gs_sweep(const double *uin, double *uout, const double *rhs, const d
 }
 
 template <int BLOCK, int K, int MODE>
-static void smooth_inst(const double *uin, double *uout, const double *rhs, const double *v1,
-                        const double *v2, const double *uc, long pitchc, long n, long pitch,
-                        Coef c, hipStream_t s) {
-    constexpr int W = 2 * (BLOCK - 2 * K);
+static int smooth_inst(const SmoothArgs &A, hipStream_t s) {
+    constexpr int W = 2 * (BLOCK - 2 * SmoothCfg<K, MODE>::H);
     static int slots = 0;   // resident workgroups of this instantiation
     if (!slots) {
         int dev = 0, cus = 0, per = 0;
@@ -817,45 +910,53 @@ static void smooth_inst(const double *uin, double *uout, const double *rhs, cons
                                                            BLOCK, 0);
         slots = std::max(1, cus) * std::max(1, per);
     }
+    const long n = A.n;
     const int strips = (int)((n + 1 + W - 1) / W);
     const long total = (long)strips * (n + 1);
-    // at least ~64 rows per workgroup so the 2S-row priming stays cheap
-    const long g = std::max<long>(1, std::min<long>(slots, total / 64));
+    // at least ~64 rows per workgroup so the priming rows stay cheap; NORM
+    // partials are bounded by the partials buffer
+    long g = std::max<long>(1, std::min<long>(slots, total / 64));
+    g = std::min<long>(g, kNormBlocks);
     const long upw = (total + g - 1) / g;
     const unsigned grid = (unsigned)((total + upw - 1) / upw);
-    MGX_LAUNCH((k_smooth<BLOCK, K, MODE>), dim3(grid), dim3(BLOCK), s, uin, uout, rhs, v1, v2,
-               uc, pitchc, (int)n, pitch, strips, upw, c);
+    MGX_LAUNCH((k_smooth<BLOCK, K, MODE>), dim3(grid), dim3(BLOCK), s, A.uin, A.uout, A.rhs, A.v1,
+               A.v2, A.uc, A.pitchc, A.rhsc, A.partials, (int)n, A.pitch, strips, upw, A.c);
+    return (int)grid;
 }
 
 template <int K, int MODE>
-static void smooth_block(const double *uin, double *uout, const double *rhs, const double *v1,
-                         const double *v2, const double *uc, long pitchc, long n, long pitch,
-                         Coef c, hipStream_t s) {
-    if (n >= 4096)
-        smooth_inst<256, K, MODE>(uin, uout, rhs, v1, v2, uc, pitchc, n, pitch, c, s);
-    else
-        smooth_inst<64, K, MODE>(uin, uout, rhs, v1, v2, uc, pitchc, n, pitch, c, s);
+static int smooth_block(const SmoothArgs &A, hipStream_t s) {
+    if (A.n >= 4096) return smooth_inst<256, K, MODE>(A, s);
+    return smooth_inst<64, K, MODE>(A, s);
 }
 
 template <int K>
-static void smooth_k(const double *uin, double *uout, const double *rhs, const double *v1,
-                     const double *v2, const double *uc, long pitchc, long n, long pitch,
-                     Coef c, int mode, hipStream_t s) {
+static int smooth_k(const SmoothArgs &A, int mode, hipStream_t s) {
     switch (mode) {
-        case 1: smooth_block<K, 1>(uin, uout, rhs, v1, v2, uc, pitchc, n, pitch, c, s); break;
-        case 2: smooth_block<K, 2>(uin, uout, rhs, v1, v2, uc, pitchc, n, pitch, c, s); break;
-        default: smooth_block<K, 0>(uin, uout, rhs, v1, v2, uc, pitchc, n, pitch, c, s); break;
+        case 0: return smooth_block<K, 0>(A, s);
+        case 1: return smooth_block<K, 1>(A, s);
+        case 2: return smooth_block<K, 2>(A, s);
+        case 4: return smooth_block<K, 4>(A, s);
+        case 5: return smooth_block<K, 5>(A, s);
+        case 8: return smooth_block<K, 8>(A, s);
+        case 9: return smooth_block<K, 9>(A, s);
+        case 10: return smooth_block<K, 10>(A, s);
+        default: return -1;
     }
 }
 
-void launch_smooth(const double *uin, double *uout, const double *rhs, const double *v1,
-                   const double *v2, const double *uc, long pitchc, long n, long pitch, Coef c,
-                   int sweeps, int mode, hipStream_t s) {
+int launch_smooth(const SmoothArgs &A, int sweeps, int mode, hipStream_t s) {
+    int blocks = -1;
     switch (sweeps) {
-        case 1: smooth_k<1>(uin, uout, rhs, v1, v2, uc, pitchc, n, pitch, c, mode, s); break;
-        case 2: smooth_k<2>(uin, uout, rhs, v1, v2, uc, pitchc, n, pitch, c, mode, s); break;
-        default: smooth_k<3>(uin, uout, rhs, v1, v2, uc, pitchc, n, pitch, c, mode, s); break;
+        case 1: blocks = smooth_k<1>(A, mode, s); break;
+        case 2: blocks = smooth_k<2>(A, mode, s); break;
+        case 3: blocks = smooth_k<3>(A, mode, s); break;
+        default: return -1;
     }
+    if (blocks > 0 && (mode & 8))
+        MGX_LAUNCH(k_norm_final, dim3(1), dim3(kFinalThreads), s, (const double *)A.partials,
+                   blocks, A.norm_out);
+    return blocks;
 }
 
 void launch_gs_colour(double *u, const double *rhs, const double *v1, const double *v2,

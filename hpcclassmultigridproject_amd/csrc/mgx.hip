@@ -143,34 +143,68 @@ int materialize(mgx_ctx *c, int l) {
     return MGX_OK;
 }
 
-// `sweeps` RB-GS sweeps (gauss_seidel, gs.cpp:109).  With prolong = true the
-// coarse correction u[l] += P(u[l+1]) (multigrid.cpp:81-83) is applied first,
-// fused into the first smoothing pass when the smoother supports it.
+// `sweeps` RB-GS sweeps (gauss_seidel, gs.cpp:109) on level l.
+//   prolong:  first apply u[l] += P(u[l+1]) (multigrid.cpp:81-83);
+//   restrict: afterwards restrict the residual into rhs[l+1] (multigrid.cpp:73-75);
+//   norm:     afterwards compute the residual norm into c->dscal[0].
+// With the temporally blocked smoother all three are fused into the first /
+// last smoothing pass; *fused_norm tells the caller whether the norm was done.
 int op_prolong_add(mgx_ctx *c, int l);
-int op_gs(mgx_ctx *c, int l, int sweeps, bool prolong = false) {
+int op_restrict(mgx_ctx *c, int l);
+int op_smooth(mgx_ctx *c, int l, int sweeps, bool prolong, bool restrict_, bool norm,
+              bool *fused_norm) {
     Level &L = c->lv[l];
-    if (c->opt.smoother == 0) {
+    if (fused_norm) *fused_norm = false;
+    if (c->opt.smoother == 0 && sweeps > 0) {
+        const int fuse = std::max(1, std::min(c->opt.fuse, mgx::kSmoothMaxSweeps));
         int done = 0;
-        while (done < sweeps || (prolong && sweeps == 0)) {
-            const int k = std::min(sweeps - done, std::max(1, std::min(c->opt.fuse, mgx::kSmoothMaxSweeps)));
-            if (k <= 0) break;
-            const bool z = L.zero;
-            const bool pr = prolong && done == 0;
+        while (done < sweeps) {
+            const int k = std::min(sweeps - done, fuse);
+            const bool first = done == 0, last = done + k == sweeps;
+            const bool pr = prolong && first && !L.zero;
+            const bool rs = restrict_ && last;
+            const bool nm = norm && last && !rs;
             if (pr) CHK(materialize(c, l + 1));
-            const int mode = z ? 1 : (pr ? 2 : 0);
-            const Level *C = pr ? &c->lv[l + 1] : nullptr;
+            int mode = 0;
+            if (L.zero) mode |= mgx::kModeZero;
+            if (pr) mode |= mgx::kModeProlong;
+            if (rs) mode |= mgx::kModeRestrict;
+            if (nm) mode |= mgx::kModeNorm;
+            mgx::SmoothArgs A{};
+            A.uin = L.u[L.cur];
+            A.uout = L.u[L.cur ^ 1];
+            A.rhs = L.rhs;
+            A.v1 = L.v1;
+            A.v2 = L.v2;
+            A.n = L.n;
+            A.pitch = L.pitch;
+            A.c = L.coef;
+            if (pr || rs) {
+                Level &Cl = c->lv[l + 1];
+                A.uc = Cl.U();
+                A.rhsc = Cl.rhs;
+                A.pitchc = Cl.pitch;
+            }
+            A.partials = c->partials;
+            A.norm_out = c->dscal;
             double bytes = 40.0 * k * L.M();
-            if (pr) bytes += 32.0 * L.M() + 8.0 * C->M();
-            CHK(launch(c, pr ? MGX_K_PSMOOTH : MGX_K_GS, l, bytes, [&] {
-                mgx::launch_smooth(L.u[L.cur], L.u[L.cur ^ 1], L.rhs, L.v1, L.v2,
-                                   C ? C->U() : nullptr, C ? C->pitch : 0, L.n, L.pitch, L.coef,
-                                   k, mode, c->stream);
-            }));
+            int kind = MGX_K_GS;
+            if (pr) {
+                bytes += 32.0 * L.M() + 8.0 * c->lv[l + 1].M();
+                kind = MGX_K_PSMOOTH;
+            }
+            if (rs) bytes += 40.0 * L.M() + 24.0 * c->lv[l + 1].M();
+            if (nm) bytes += 48.0 * L.M();
+            int blocks = 0;
+            CHK(launch(c, kind, l, bytes, [&] { blocks = mgx::launch_smooth(A, k, mode, c->stream); }));
+            if (blocks < 0) return fail(MGX_E_ARG, "launch_smooth: unsupported sweeps/mode");
             L.cur ^= 1;
             L.zero = false;
+            if (rs) c->lv[l + 1].zero = true;
+            if (nm && fused_norm) *fused_norm = true;
             done += k;
         }
-        if (prolong && sweeps == 0) CHK(op_prolong_add(c, l));
+        if (prolong && L.zero) CHK(op_prolong_add(c, l));   // unreachable in practice
         return MGX_OK;
     }
     if (prolong) CHK(op_prolong_add(c, l));
@@ -193,11 +227,23 @@ int op_gs(mgx_ctx *c, int l, int sweeps, bool prolong = false) {
             }));
         }
     }
+    if (restrict_) CHK(op_restrict(c, l));
     return MGX_OK;
+}
+
+int op_gs(mgx_ctx *c, int l, int sweeps) {
+    return op_smooth(c, l, sweeps, false, false, false, nullptr);
 }
 
 // residual + compute_norm on level l, norm read back to the host (the one
 // host sync per cycle, gs.cpp:86 / multigrid.cpp:105,113).
+int read_norm(mgx_ctx *c, double *norm) {
+    HIPCHK(hipMemcpyAsync(c->hscal, c->dscal, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    *norm = c->hscal[0];
+    return MGX_OK;
+}
+
 int op_residual_norm(mgx_ctx *c, int l, double *norm, double bytes_per_pt = 48.0) {
     CHK(materialize(c, l));
     Level &L = c->lv[l];
@@ -205,10 +251,7 @@ int op_residual_norm(mgx_ctx *c, int l, double *norm, double bytes_per_pt = 48.0
         mgx::launch_residual_norm(L.U(), L.rhs, L.v1, L.v2, L.n, L.pitch, L.coef, c->partials,
                                   c->dscal, c->stream);
     }));
-    HIPCHK(hipMemcpyAsync(c->hscal, c->dscal, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    *norm = c->hscal[0];
-    return MGX_OK;
+    return read_norm(c, norm);
 }
 
 // residual -> restriction into rhs[l+1]; u[l+1] = 0 (multigrid.cpp:73-77).
@@ -250,25 +293,39 @@ int op_coarse(mgx_ctx *c, int l) {
     int it = 0;
     double res = 1.0;
     while (it < c->opt.coarse_maxit && res > c->opt.coarse_tol) {
-        CHK(op_gs(c, l, 1));
-        CHK(op_residual_norm(c, l, &res, 48.0));
+        bool fused = false;
+        CHK(op_smooth(c, l, 1, false, false, true, &fused));
+        if (fused)
+            CHK(read_norm(c, &res));
+        else
+            CHK(op_residual_norm(c, l, &res, 48.0));
         ++it;
     }
     c->hscal[4] += it;
     return MGX_OK;
 }
 
-// mg_inner (multigrid.cpp:17-92).
-int op_vcycle(mgx_ctx *c, int l) {
+// mg_inner (multigrid.cpp:17-92).  If norm != nullptr (finest level only) the
+// residual norm after the cycle (multigrid.cpp:112-113) is produced too, fused
+// into the last post-smoothing pass when possible.
+int op_vcycle(mgx_ctx *c, int l, double *norm = nullptr) {
+    bool have_norm = false;
     for (int sh = 0; sh < c->opt.shape; ++sh) {
+        const bool last = sh == c->opt.shape - 1;
         if (l == c->L - 1) {
             CHK(op_coarse(c, l));
         } else {
-            CHK(op_gs(c, l, c->opt.nsmooth));
-            CHK(op_restrict(c, l));
+            CHK(op_smooth(c, l, c->opt.nsmooth, false, /*restrict=*/true, false, nullptr));
             CHK(op_vcycle(c, l + 1));
-            CHK(op_gs(c, l, c->opt.nsmooth, /*prolong=*/true));
+            CHK(op_smooth(c, l, c->opt.nsmooth, /*prolong=*/true, false, norm && last,
+                          &have_norm));
         }
+    }
+    if (norm) {
+        if (have_norm)
+            CHK(read_norm(c, norm));
+        else
+            CHK(op_residual_norm(c, l, norm));
     }
     return MGX_OK;
 }
@@ -287,10 +344,7 @@ int op_mg_outer(mgx_ctx *c, double tol, int *cycles, double *res0_out, double *r
     CHK(op_residual_norm(c, 0, &res0));
     res = res0;
     int iter = 0;
-    for (; iter < c->opt.max_cycle && res / res0 > tol; ++iter) {
-        CHK(op_vcycle(c, 0));
-        CHK(op_residual_norm(c, 0, &res));
-    }
+    for (; iter < c->opt.max_cycle && res / res0 > tol; ++iter) CHK(op_vcycle(c, 0, &res));
     if (cycles) *cycles = iter;
     if (res0_out) *res0_out = res0;
     if (res_out) *res_out = res;
@@ -600,10 +654,7 @@ int mgx_step(mgx_ctx *c, double tol, int *cycles) {
 int mgx_run_cycles(mgx_ctx *c, int cycles, double *res) {
     if (!c || cycles < 0) return fail(MGX_E_ARG, "mgx_run_cycles: bad args");
     double r = 0;
-    for (int k = 0; k < cycles; ++k) {
-        CHK(op_vcycle(c, 0));
-        CHK(op_residual_norm(c, 0, &r));
-    }
+    for (int k = 0; k < cycles; ++k) CHK(op_vcycle(c, 0, &r));
     if (res) *res = r;
     return MGX_OK;
 }
