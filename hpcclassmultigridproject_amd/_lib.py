@@ -76,6 +76,8 @@ _SIGS = {
     "mgx_profile_enable": (_I, [_vp, _I]),
     "mgx_profile_reset": (_I, [_vp]),
     "mgx_profile_get": (_I, [_vp, _I, _I, C.POINTER(_L), _dp, _dp]),
+    "mgx_set_tuning": (_I, [C.c_char_p, _L]),
+    "mgx_get_tuning": (_I, [C.c_char_p, C.POINTER(_L)]),
 }
 
 _lib = None
@@ -111,3 +113,13 @@ def default_options(**kw) -> Options:
             raise TypeError(f"unknown option {k}")
         setattr(o, k, v)
     return o
+
+
+def set_tuning(key: str, value: int):
+    check(lib().mgx_set_tuning(key.encode(), value))
+
+
+def get_tuning(key: str) -> int:
+    v = C.c_long()
+    check(lib().mgx_get_tuning(key.encode(), C.byref(v)))
+    return v.value

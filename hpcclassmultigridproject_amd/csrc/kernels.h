@@ -68,6 +68,11 @@ struct SmoothArgs {
     double *norm_out;   // NORM
 };
 int launch_smooth(const SmoothArgs &a, int sweeps, int mode, hipStream_t s);
+// Levels with n <= tile_max_n use the 2-D tile form of the fused pass (small
+// levels: latency bound), larger ones the row march.  Default 2048, or the
+// MGX_TILE_MAX_N environment variable.
+void set_tile_max_n(long v);
+long get_tile_max_n();
 // One colour, in place (two launches make a sweep).  Reference for A/B timing.
 void launch_gs_colour(double *u, const double *rhs, const double *v1, const double *v2,
                       long n, long pitch, Coef c, int colour, hipStream_t s);

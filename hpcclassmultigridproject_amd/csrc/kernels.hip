@@ -10,6 +10,7 @@
 #include "kernels.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace mgx {
 
@@ -619,6 +620,146 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
     }
 }
 
+// k_smooth_tile: the same fused pass (K sweeps + optional prolong / restrict
+// / norm) for SMALL levels, where the serial row march of k_smooth is latency
+// bound.  A workgroup owns a TR x TC output tile and loads it with an EH-wide
+// halo (EH = E rounded up to even, so the tile origin has even parity) into
+// LDS; all stages then run as parallel colour updates over the whole
+// extended tile with one barrier between stages.  The exact region shrinks
+// by one point per stage, so the output tile is exact (same argument as
+// k_smooth).  Each lane owns fixed column pairs of the tile and keeps their
+// rhs / v1 / v2 in registers for all stages.
+template <int K, int MODE>
+struct TileCfg {
+    using C = SmoothCfg<K, MODE>;
+    static constexpr int TR = 16, TC = 64;               // output tile
+    static constexpr int EH = (C::E + 1) / 2 * 2;         // halo, even
+    static constexpr int RT = TR + 2 * EH, WT = TC + 2 * EH;
+    static constexpr int PAIRS = RT * WT / 2;
+    static constexpr int THREADS = 256;
+    static constexpr int PPT = (PAIRS + THREADS - 1) / THREADS;   // pairs per thread
+};
+
+template <int K, int MODE>
+__global__ __launch_bounds__(256) void k_smooth_tile(
+    const double *__restrict__ uin, double *__restrict__ uout, const double *__restrict__ rhs,
+    const double *__restrict__ v1, const double *__restrict__ v2, const double *__restrict__ uc,
+    long pitchc, double *__restrict__ rhsc, double *__restrict__ partials, int n, long pitch,
+    int tiles_x, Coef c) {
+    using C = SmoothCfg<K, MODE>;
+    using T = TileCfg<K, MODE>;
+    constexpr int S = C::S, EH = T::EH, WT = T::WT, PPT = T::PPT, HW = WT / 2;
+    __shared__ __attribute__((aligned(16))) double tu[T::RT * WT];
+
+    const int t = threadIdx.x;
+    const int ty = blockIdx.x / tiles_x, tx = blockIdx.x % tiles_x;
+    const long i0 = (long)ty * T::TR - EH, j0 = (long)tx * T::TC - EH;   // tile origin (even)
+    const int nc = n >> 1;
+
+    // rhs / v1 / v2 of the lane's pairs as scalar arrays (static indices only,
+    // so they stay in registers)
+    double f0[PPT], f1[PPT], x0[PPT], x1[PPT], y0[PPT], y1[PPT];
+    bool ok[PPT];
+#pragma unroll
+    for (int m = 0; m < PPT; ++m) {
+        const int q = t + m * 256;
+        ok[m] = false;
+        f0[m] = f1[m] = x0[m] = x1[m] = y0[m] = y1[m] = 0.0;
+        if (q >= T::PAIRS) continue;
+        const int r = q / HW, k = q % HW;
+        const long gi = i0 + r, gj = j0 + 2 * k;
+        double2 v = make_double2(0.0, 0.0);
+        if (gi >= 0 && gi <= n && gj >= 0 && gj <= n) {
+            ok[m] = true;
+            const long o = gi * pitch + gj;
+            if (!C::ZERO) v = ld2(uin + o);
+            if (C::PROL) {
+                const long ii = gi >> 1, jj = gj >> 1;
+                const double *p0 = uc + ii * pitchc + jj;
+                const double q00 = p0[0], q01 = (jj + 1 <= nc) ? p0[1] : 0.0;
+                double2 pr;
+                if (!(gi & 1)) {
+                    pr.x = q00;
+                    pr.y = (q00 + q01) / 2;
+                } else {
+                    const double q10 = p0[pitchc], q11 = (jj + 1 <= nc) ? p0[pitchc + 1] : 0.0;
+                    pr.x = (q00 + q10) / 2;
+                    pr.y = (q00 + q10 + q01 + q11) / 4;
+                }
+                v.x = v.x + pr.x;
+                v.y = v.y + pr.y;
+            }
+            const double2 rr = ld2(rhs + o), xx = ld2(v1 + o), yy = ld2(v2 + o);
+            f0[m] = rr.x;
+            f1[m] = rr.y;
+            x0[m] = xx.x;
+            x1[m] = xx.y;
+            y0[m] = yy.x;
+            y1[m] = yy.y;
+        }
+        st2(&tu[r * WT + 2 * k], v);
+    }
+    __syncthreads();
+
+#pragma unroll
+    for (int h = 0; h < S; ++h) {
+#pragma unroll
+        for (int m = 0; m < PPT; ++m) {
+            const int q = t + m * 256;
+            if (q >= T::PAIRS || !ok[m]) continue;
+            const int r = q / HW, k = q % HW;
+            const long gi = i0 + r;
+            const int cs = (r & 1) ^ (h & 1);   // origin parity is even
+            const long gj = j0 + 2 * k + cs;
+            if (gi < 1 || gi > n - 1 || gj < 1 || gj > n - 1) continue;
+            if (r < 1 || r > T::RT - 2 || (2 * k + cs) < 1 || (2 * k + cs) > WT - 2) continue;
+            const int x = r * WT + 2 * k + cs;
+            const double fr = cs ? f1[m] : f0[m], fx = cs ? x1[m] : x0[m],
+                         fy = cs ? y1[m] : y0[m];
+            tu[x] = gs_point_fast(fr, fx, fy, tu[x - WT], tu[x - 1], tu[x + WT], tu[x + 1], c);
+        }
+        __syncthreads();
+    }
+
+    double acc = 0.0;
+#pragma unroll
+    for (int m = 0; m < PPT; ++m) {
+        const int q = t + m * 256;
+        if (q >= T::PAIRS || !ok[m]) continue;
+        const int r = q / HW, k = q % HW;
+        if (r < EH || r >= EH + T::TR || 2 * k < EH || 2 * k >= EH + T::TC) continue;
+        const long gi = i0 + r, gj = j0 + 2 * k;
+        const int x = r * WT + 2 * k;
+        st2(uout + gi * pitch + gj, ld2(&tu[x]));
+        if (C::REST || C::NORM) {
+            const bool in0 = gi >= 1 && gi <= n - 1 && gj >= 1 && gj <= n - 1;
+            const bool in1 = gi >= 1 && gi <= n - 1 && gj + 1 <= n - 1;
+            if (C::REST) {
+                if (!(gi & 1) && in0 && gi <= n - 2 && gj <= n - 2)
+                    rhsc[(gi >> 1) * pitchc + (gj >> 1)] =
+                        res_point(f0[m], x0[m], y0[m], tu[x], tu[x - WT], tu[x - 1], tu[x + WT],
+                                  tu[x + 1], c);
+            } else {
+                if (in0) {
+                    const double res = res_point(f0[m], x0[m], y0[m], tu[x], tu[x - WT],
+                                                 tu[x - 1], tu[x + WT], tu[x + 1], c);
+                    acc += res * res;
+                }
+                if (in1) {
+                    const double res = res_point(f1[m], x1[m], y1[m], tu[x + 1], tu[x + 1 - WT],
+                                                 tu[x], tu[x + 1 + WT], tu[x + 2], c);
+                    acc += res * res;
+                }
+            }
+        }
+    }
+    if (C::NORM) {
+        __shared__ double red_lds[4];
+        const double tot = block_sum(acc, red_lds);
+        if (t == 0) partials[blockIdx.x] = tot;
+    }
+}
+
 // One colour in place (two launches = one sweep).  Grid (strips, interior rows).
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void k_gs_colour(double *u, const double *rhs,
@@ -924,8 +1065,41 @@ static int smooth_inst(const SmoothArgs &A, hipStream_t s) {
     return (int)grid;
 }
 
+long g_tile_max_n = -1;   // levels with n <= this use k_smooth_tile
+
+void set_tile_max_n(long v) { g_tile_max_n = v; }
+long get_tile_max_n();
+
+static long tile_max_n() {
+    if (g_tile_max_n < 0) {
+        const char *e = getenv("MGX_TILE_MAX_N");
+        g_tile_max_n = e ? atol(e) : 2048;
+    }
+    return g_tile_max_n;
+}
+
+long get_tile_max_n() { return tile_max_n(); }
+
+template <int K, int MODE>
+static int smooth_tile_inst(const SmoothArgs &A, hipStream_t s) {
+    using T = TileCfg<K, MODE>;
+    const long n = A.n;
+    const int tiles_x = (int)((n + 1 + T::TC - 1) / T::TC);
+    const int tiles_y = (int)((n + 1 + T::TR - 1) / T::TR);
+    const long grid = (long)tiles_x * tiles_y;
+    if ((MODE & 8) && grid > kNormBlocks) return -1;
+    MGX_LAUNCH((k_smooth_tile<K, MODE>), dim3((unsigned)grid), dim3(256), s, A.uin, A.uout,
+               A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, A.partials, (int)n, A.pitch, tiles_x,
+               A.c);
+    return (int)grid;
+}
+
 template <int K, int MODE>
 static int smooth_block(const SmoothArgs &A, hipStream_t s) {
+    if (A.n <= tile_max_n()) {
+        const int g = smooth_tile_inst<K, MODE>(A, s);
+        if (g > 0) return g;
+    }
     if (A.n >= 4096) return smooth_inst<256, K, MODE>(A, s);
     return smooth_inst<64, K, MODE>(A, s);
 }

@@ -790,3 +790,21 @@ extern "C" int mgx_init_problem(double *u0, double *v1, double *v2, long N, int 
     }
     return MGX_OK;
 }
+
+// ---- tuning knobs (process-wide)
+extern "C" int mgx_set_tuning(const char *key, long value) {
+    if (!key) return fail(MGX_E_ARG, "mgx_set_tuning: null key");
+    if (!strcmp(key, "tile_max_n")) {
+        mgx::set_tile_max_n(value);
+        return MGX_OK;
+    }
+    return fail(MGX_E_ARG, std::string("mgx_set_tuning: unknown key ") + key);
+}
+extern "C" int mgx_get_tuning(const char *key, long *value) {
+    if (!key || !value) return fail(MGX_E_ARG, "mgx_get_tuning: null argument");
+    if (!strcmp(key, "tile_max_n")) {
+        *value = mgx::get_tile_max_n();
+        return MGX_OK;
+    }
+    return fail(MGX_E_ARG, std::string("mgx_get_tuning: unknown key ") + key);
+}

@@ -153,6 +153,12 @@ int mgx_coarse_iterations(mgx_ctx *ctx, long *iters);
 int mgx_stream(mgx_ctx *ctx, void **stream);
 int mgx_synchronize(mgx_ctx *ctx);
 
+/* Process-wide tuning knobs.  "tile_max_n": levels with n <= value run the
+ * fused smoothing pass as 2-D LDS tiles instead of the row march (default 2048;
+ * env MGX_TILE_MAX_N). */
+int mgx_set_tuning(const char *key, long value);
+int mgx_get_tuning(const char *key, long *value);
+
 /* Per-kernel timing with HIP events on the context stream. */
 #define MGX_K_GS 0             /* RB-GS sweep (one full red+black sweep) */
 #define MGX_K_RESTRICT 1       /* residual restricted to the coarse rhs */

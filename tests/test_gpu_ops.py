@@ -101,9 +101,19 @@ def test_context_tower_matches_oracle(oracle_mod, tower_mode):
 SMOOTHERS = [(0, 3), (0, 2), (0, 1), (1, 3), (2, 3)]   # (smoother, sweeps fused per pass)
 
 
+@pytest.fixture(params=[2048, 0], ids=["tile", "march"])
+def tile_mode(request):
+    """Small levels as 2-D LDS tiles (default) or as the row march."""
+    from hpcclassmultigridproject_amd import _lib
+    old = _lib.get_tuning("tile_max_n")
+    _lib.set_tuning("tile_max_n", request.param)
+    yield request.param
+    _lib.set_tuning("tile_max_n", old)
+
+
 @pytest.mark.parametrize("smoother,fuse", SMOOTHERS)
-@pytest.mark.parametrize("N", [16, 128, 512, 4096, 8192])
-def test_context_gs_bitwise_vs_oracle(oracle_mod, N, smoother, fuse):
+@pytest.mark.parametrize("N", [16, 128, 512, 2048, 4096, 8192])
+def test_context_gs_bitwise_vs_oracle(oracle_mod, N, smoother, fuse, tile_mode):
     """Temporally blocked passes (0), two-colour passes (1) and one-pass single
     sweeps (2) all equal 3 x gs.cpp:109 bitwise."""
     O = oracle_mod

@@ -30,8 +30,17 @@ def test_timestepper_bitwise_vs_reference(tag):
     assert np.array_equal(uT, g["uT"])
 
 
+@pytest.fixture(params=[2048, 0], ids=["tile", "march"])
+def tile_mode(request):
+    from hpcclassmultigridproject_amd import _lib
+    old = _lib.get_tuning("tile_max_n")
+    _lib.set_tuning("tile_max_n", request.param)
+    yield request.param
+    _lib.set_tuning("tile_max_n", old)
+
+
 @pytest.mark.parametrize("smoother,fuse", [(0, 3), (0, 2), (0, 1), (1, 3), (2, 3)])
-def test_vcycle_bitwise_vs_reference_N256(smoother, fuse):
+def test_vcycle_bitwise_vs_reference_N256(smoother, fuse, tile_mode):
     g = load_golden("vcycle_N256_L4.npz")
     N, maxlvl, nu, dt = g["params"]
     N, maxlvl = int(N), int(maxlvl)
@@ -104,7 +113,7 @@ def test_two_timesteps_N16384(golden_summary):
     (256, 7, 1, 1, 0),      # coarsest n = 4
     (2048, 2, 3, 1, 0),     # large coarsest level (host-loop coarse solve)
 ])
-def test_mg_outer_bitwise_vs_oracle(oracle_mod, N, maxlvl, nsmooth, shape, tower):
+def test_mg_outer_bitwise_vs_oracle(oracle_mod, N, maxlvl, nsmooth, shape, tower, tile_mode):
     O = oracle_mod
     O.set_threads(8)
     try:
