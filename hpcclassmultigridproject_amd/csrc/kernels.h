@@ -73,6 +73,9 @@ int launch_smooth(const SmoothArgs &a, int sweeps, int mode, hipStream_t s);
 // MGX_TILE_MAX_N environment variable.
 void set_tile_max_n(long v);
 long get_tile_max_n();
+// Workgroup width (lanes) of the row march on levels with n >= 4096: 128 or 256.
+void set_march_block(long v);
+long get_march_block();
 // One colour, in place (two launches make a sweep).  Reference for A/B timing.
 void launch_gs_colour(double *u, const double *rhs, const double *v1, const double *v2,
                       long n, long pitch, Coef c, int colour, hipStream_t s);

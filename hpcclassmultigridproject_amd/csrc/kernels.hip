@@ -381,7 +381,9 @@ __global__ __launch_bounds__(BLOCK) void k_gs_sweep(const double *__restrict__ u
 // bitwise that of K reference sweeps.
 //
 // rhs / v1 / v2 of a row stay in registers from the step they are loaded to
-// the last stage that needs them.  The step loop is unrolled by NS = S+2
+// the last stage that needs them; they are loaded two steps before their
+// first use into the one ring slot that dies each step, and u rows are
+// prefetched two steps ahead too (two alternating register sets).  The step loop is unrolled by NS = S+2
 // (even), and its start aligned to NS, so every register-ring index and the
 // parity of every row are compile-time constants: no selects, static LDS
 // offsets.  Ring slots are scalar (SALU) arithmetic.
@@ -457,8 +459,8 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
         const int b = (int)min((long)(n + 1), (long)a + (end - start));
         start += b - a;
 
-        const long j0 = (long)strip * W;
-        const long c0 = j0 - 2 * H + 2 * l;
+        const int j0 = strip * W;
+        const int c0 = j0 - 2 * H + 2 * l;   // lane column (32-bit: the row base is scalar)
         const bool act = c0 >= 0 && c0 <= n;
         const bool keep = act && l >= H && l < BLOCK - H;
         // per-lane interior flags of the two columns of the pair
@@ -466,37 +468,43 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
         const bool in1 = act && c0 + 1 <= n - 1;
         const int x0 = 1 + 2 * l;
 
-        // prefetched u row (+ coarse operands of its prolongation)
-        double2 X = make_double2(0.0, 0.0);
-        double q00 = 0.0, q01 = 0.0, q10 = 0.0, q11 = 0.0;
-        int xrow = 0;
-        auto load_u = [&](int R) {
-            xrow = R;
+        // Prefetched u rows (+ coarse operands of their prolongation): row R
+        // lives in set R & 1 from its load at step R-5 to its LDS store at step
+        // R-3 (prefetch distance 2).  s == p (mod 2), so the set is static.
+        struct UPre {
+            double2 X;
+            double q00, q01, q10, q11;
+        };
+        UPre up[2];
+        up[0] = up[1] = UPre{make_double2(0.0, 0.0), 0.0, 0.0, 0.0, 0.0};
+        auto load_u = [&](int R, UPre &u) {
             if (C::ZERO || !act || R < 0 || R > n) return;
-            X = ld2(uin + (long)R * pitch + c0);
+            u.X = ld2((uin + (long)R * pitch) + c0);
             if (C::PROL) {
-                const long i = R >> 1, j = c0 >> 1;
-                const double *p0 = uc + i * pitchc + j;
-                q00 = p0[0];
-                q01 = (j + 1 <= nc) ? p0[1] : 0.0;
-                if (R & 1) {
-                    q10 = p0[pitchc];
-                    q11 = (j + 1 <= nc) ? p0[pitchc + 1] : 0.0;
-                }
+                // branch-free: even rows read coarse row R/2 twice (cache hits)
+                const int j = c0 >> 1;
+                const double *p0 = (uc + (long)(R >> 1) * pitchc) + j;
+                const double *p1 = p0 + ((R & 1) ? pitchc : 0);
+                const int j1 = (j + 1 <= nc) ? 1 : 0;
+                u.q00 = p0[0];
+                u.q01 = p0[j1];
+                u.q10 = p1[0];
+                u.q11 = p1[j1];
             }
         };
-        auto put_u = [&](int sl) {
-            const int R = xrow;
-            double2 v = X;
+        auto put_u = [&](int R, int sl, const UPre &u) {
+            double2 v = u.X;
             if (C::ZERO) v = make_double2(0.0, 0.0);
             if (C::PROL && act && R >= 0 && R <= n) {
                 double2 pr;
+                const double q01 = (c0 >> 1) + 1 <= nc ? u.q01 : 0.0;
+                const double q11 = (c0 >> 1) + 1 <= nc ? u.q11 : 0.0;
                 if (!(R & 1)) {
-                    pr.x = q00;
-                    pr.y = (q00 + q01) / 2;
+                    pr.x = u.q00;
+                    pr.y = (u.q00 + q01) / 2;
                 } else {
-                    pr.x = (q00 + q10) / 2;
-                    pr.y = (q00 + q10 + q01 + q11) / 4;
+                    pr.x = (u.q00 + u.q10) / 2;
+                    pr.y = (u.q00 + u.q10 + q01 + q11) / 4;
                 }
                 v.x = v.x + pr.x;
                 v.y = v.y + pr.y;
@@ -505,10 +513,10 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
         };
         auto load_rv = [&](int R, RowData &d) {
             if (!act || R < 0 || R > n) return;
-            const long o = (long)R * pitch + c0;
-            d.r = ld2(rhs + o);
-            d.x = ld2(v1 + o);
-            d.y = ld2(v2 + o);
+            const long o = (long)R * pitch;   // scalar row offset
+            d.r = ld2((rhs + o) + c0);
+            d.x = ld2((v1 + o) + c0);
+            d.y = ld2((v2 + o) + c0);
         };
 
         const int s_first = a - E;
@@ -524,16 +532,19 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
         RowData rd[NS];
 #pragma unroll
         for (int q = 0; q < NS; ++q) rd[q].r = rd[q].x = rd[q].y = make_double2(0.0, 0.0);
-        // prologue: ring rows s..s+2, X = u row s+3, rd[1] = rhs/v row s+1
+        // prologue (s even): ring rows s..s+2; u rows s+3, s+4 in flight (sets 1,
+        // 0); rhs/v rows s+1, s+2 in rd[1], rd[2]
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-            load_u(s + d);
+            load_u(s + d, up[0]);
             int sl = base + d;
             sl -= sl >= NR ? NR : 0;
-            put_u(sl);
+            put_u(s + d, sl, up[0]);
         }
-        load_u(s + 3);
+        load_u(s + 3, up[1]);
+        load_u(s + 4, up[0]);
         load_rv(s + 1, rd[1]);
+        load_rv(s + 2, rd[2]);
         __syncthreads();
 
         for (;;) {
@@ -546,10 +557,9 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
                     if (d < 0) t += t < 0 ? NR : 0;
                     return t;
                 };
-                // (1) u row s+3 into the ring, prefetch u row s+4 and rhs/v row s+2
-                put_u(slot(3));
-                load_u(s + 4);
-                load_rv(s + 2, rd[(p + 2) % NS]);
+                // (1) u row s+3 into the ring; its prefetch set takes u row s+5
+                put_u(s + 3, slot(3), up[(p + 1) & 1]);
+                load_u(s + 5, up[(p + 1) & 1]);
                 // (2) the S smoothing stages
 #pragma unroll
                 for (int h = 0; h < S; ++h) {
@@ -572,7 +582,7 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
                 {
                     const int ro = s + 2 - S;
                     if (keep && ro >= a && ro < b)
-                        st2(uout + (long)ro * pitch + c0, ld2(&ring[slot(2 - S)][x0]));
+                        st2((uout + (long)ro * pitch) + c0, ld2(&ring[slot(2 - S)][x0]));
                 }
                 // (4) residual stage on row s+1-S
                 if (C::REST || C::NORM) {
@@ -587,7 +597,7 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
                                 const double res =
                                     res_point(d.r.x, d.x.x, d.y.x, rm[x0], rn_[x0], rm[x0 - 1],
                                               rs_[x0], rm[x0 + 1], c);
-                                rhsc[(long)(r >> 1) * pitchc + (c0 >> 1)] = res;
+                                (rhsc + (long)(r >> 1) * pitchc)[c0 >> 1] = res;
                             }
                         } else {
                             if (in0) {
@@ -605,6 +615,9 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
                         }
                     }
                 }
+                // (5) rhs/v row s+3 into the slot of row s+1-S, whose last use
+                // (the residual stage, or stage S-1 one step ago) is done
+                load_rv(s + 3, rd[(p + 3) % NS]);
                 ++base;
                 base -= base >= NR ? NR : 0;
                 if (++s > s_last) goto done;
@@ -1094,13 +1107,28 @@ static int smooth_tile_inst(const SmoothArgs &A, hipStream_t s) {
     return (int)grid;
 }
 
+long g_march_block = -1;   // workgroup width of the row march for n >= 4096
+
+static long march_block() {
+    if (g_march_block < 0) {
+        const char *e = getenv("MGX_MARCH_BLOCK");
+        g_march_block = e ? atol(e) : 256;
+    }
+    return g_march_block;
+}
+void set_march_block(long v) { g_march_block = v; }
+long get_march_block() { return march_block(); }
+
 template <int K, int MODE>
 static int smooth_block(const SmoothArgs &A, hipStream_t s) {
     if (A.n <= tile_max_n()) {
         const int g = smooth_tile_inst<K, MODE>(A, s);
         if (g > 0) return g;
     }
-    if (A.n >= 4096) return smooth_inst<256, K, MODE>(A, s);
+    if (A.n >= 4096) {
+        if (march_block() == 128) return smooth_inst<128, K, MODE>(A, s);
+        return smooth_inst<256, K, MODE>(A, s);
+    }
     return smooth_inst<64, K, MODE>(A, s);
 }
 

@@ -798,12 +798,21 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgx::set_tile_max_n(value);
         return MGX_OK;
     }
+    if (!strcmp(key, "march_block")) {
+        if (value != 128 && value != 256) return fail(MGX_E_ARG, "march_block must be 128 or 256");
+        mgx::set_march_block(value);
+        return MGX_OK;
+    }
     return fail(MGX_E_ARG, std::string("mgx_set_tuning: unknown key ") + key);
 }
 extern "C" int mgx_get_tuning(const char *key, long *value) {
     if (!key || !value) return fail(MGX_E_ARG, "mgx_get_tuning: null argument");
     if (!strcmp(key, "tile_max_n")) {
         *value = mgx::get_tile_max_n();
+        return MGX_OK;
+    }
+    if (!strcmp(key, "march_block")) {
+        *value = mgx::get_march_block();
         return MGX_OK;
     }
     return fail(MGX_E_ARG, std::string("mgx_get_tuning: unknown key ") + key);

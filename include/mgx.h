@@ -155,7 +155,8 @@ int mgx_synchronize(mgx_ctx *ctx);
 
 /* Process-wide tuning knobs.  "tile_max_n": levels with n <= value run the
  * fused smoothing pass as 2-D LDS tiles instead of the row march (default 2048;
- * env MGX_TILE_MAX_N). */
+ * env MGX_TILE_MAX_N).  "march_block": lanes per workgroup of the row march on
+ * levels with n >= 4096, 128 or 256 (default 256; env MGX_MARCH_BLOCK). */
 int mgx_set_tuning(const char *key, long value);
 int mgx_get_tuning(const char *key, long *value);
 
