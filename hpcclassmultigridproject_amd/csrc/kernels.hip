@@ -477,15 +477,21 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
         };
         UPre up[2];
         up[0] = up[1] = UPre{make_double2(0.0, 0.0), 0.0, 0.0, 0.0, 0.0};
+        // Loads are issued unconditionally, with row and column clamped into
+        // the array: a conditional load makes the waitcnt pass fall back to
+        // vmcnt(0) and drain the whole prefetch queue.  Values loaded for rows
+        // or lanes outside the domain are never used.
+        const int cl = min(max(c0, 0), (int)pitch - 2);   // clamped lane column
+        const int jl = cl >> 1;                            // its coarse column
+        const int j1 = (jl + 1 <= nc) ? 1 : 0;
         auto load_u = [&](int R, UPre &u) {
-            if (C::ZERO || !act || R < 0 || R > n) return;
-            u.X = ld2((uin + (long)R * pitch) + c0);
+            if (C::ZERO) return;
+            const int Rc = min(max(R, 0), n);
+            u.X = ld2((uin + (long)Rc * pitch) + cl);
             if (C::PROL) {
                 // branch-free: even rows read coarse row R/2 twice (cache hits)
-                const int j = c0 >> 1;
-                const double *p0 = (uc + (long)(R >> 1) * pitchc) + j;
-                const double *p1 = p0 + ((R & 1) ? pitchc : 0);
-                const int j1 = (j + 1 <= nc) ? 1 : 0;
+                const double *p0 = (uc + (long)(Rc >> 1) * pitchc) + jl;
+                const double *p1 = p0 + ((Rc & 1) ? pitchc : 0);
                 u.q00 = p0[0];
                 u.q01 = p0[j1];
                 u.q10 = p1[0];
@@ -497,8 +503,8 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
             if (C::ZERO) v = make_double2(0.0, 0.0);
             if (C::PROL && act && R >= 0 && R <= n) {
                 double2 pr;
-                const double q01 = (c0 >> 1) + 1 <= nc ? u.q01 : 0.0;
-                const double q11 = (c0 >> 1) + 1 <= nc ? u.q11 : 0.0;
+                const double q01 = j1 ? u.q01 : 0.0;
+                const double q11 = j1 ? u.q11 : 0.0;
                 if (!(R & 1)) {
                     pr.x = u.q00;
                     pr.y = (u.q00 + q01) / 2;
@@ -512,11 +518,10 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
             st2(&ring[sl][x0], v);
         };
         auto load_rv = [&](int R, RowData &d) {
-            if (!act || R < 0 || R > n) return;
-            const long o = (long)R * pitch;   // scalar row offset
-            d.r = ld2((rhs + o) + c0);
-            d.x = ld2((v1 + o) + c0);
-            d.y = ld2((v2 + o) + c0);
+            const long o = (long)min(max(R, 0), n) * pitch;   // scalar row offset
+            d.r = ld2((rhs + o) + cl);
+            d.x = ld2((v1 + o) + cl);
+            d.y = ld2((v2 + o) + cl);
         };
 
         const int s_first = a - E;
