@@ -6,7 +6,15 @@ OUT=${1:-gpurun_out/pmc}
 shift || true
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
+CGROUPS=(
+  "FETCH_SIZE"
+  "WRITE_SIZE"
+  "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU"
+  "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA"
+  "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum"
+  "GRBM_GUI_ACTIVE GRBM_COUNT"
+)
+for grp in "${CGROUPS[@]}"; do
   tag=$(echo $grp | cut -d' ' -f1)
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d "$OUT/$tag" -o run --output-format csv -- python3 tools/pmc_vcycle.py "$@" > "$OUT/$tag.log" 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d "$OUT/$tag" -o run --output-format csv -- python3 tools/pmc_vcycle.py "$@" > "$OUT/$tag.log" 2>&1 || echo "group $tag failed"
 done
