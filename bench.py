@@ -11,9 +11,12 @@ rotating velocity, nu=-4e-4, dt=dx/10) at N=16384, L=9 levels (coarsest 64),
 3 pre/post RB-GS sweeps, fp64; inputs resident in HBM before the timed region.
 
 value = (N-1)^2 * steps * ranks / max-over-ranks seconds.
-roofline: the dominant kernel is the fused RB-GS sweep on the finest level;
-achieved = 40 B x (N+1)^2 algorithmic bytes per launch / its mean duration
-(HIP events on the context stream, inside the timed region).
+roofline: the dominant kernel (largest device time: a finest-level fused
+smoothing pass) with achieved = its algorithmic bytes per launch (SURVEY 8d:
+40 B/point per RB sweep x 3 sweeps + the fused residual/restriction or
+prolongation/norm work) / its mean duration (HIP events on the context stream,
+inside the timed region); traffic = its measured HBM bytes per launch
+(rocprofv3 PMC, profiles/r1_hbm_traffic.json).
 cpu_baseline: rank 0, N=1 only: the reference's own mg_inner (oracle/_ref,
 built from the unmodified sources with the reference Makefile flags), one
 V-cycle of the same workload, OpenMP tasks on the host cores.
@@ -30,7 +33,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s HBM3E
-GS_BYTES_PER_PT = 40.0  # read u, rhs, v1, v2; write u
+# (kind, level) -> kernel instance of the default config, for the PMC traffic
+# summary committed under profiles/ (tools/pmc_collect.sh, tools/pmc_summary.py)
+KERNEL_IDS = {(0, 0): "mgx::k_smooth<256, 3, 4> grid=196608",
+              (7, 0): "mgx::k_smooth<256, 3, 10> grid=196608"}
 
 
 def parse():
@@ -147,22 +153,42 @@ def main():
                 nl, msl, bl = mg.profile_get(kind, lvl)
                 if nl:
                     kernels[name][f"L{lvl}_ms_per_step"] = round(msl / args.steps, 4)
-    n0, ms0, b0 = mg.profile_get(_lib.K_GS, 0)
+    # dominant kernel = the (kind, level) with the largest device time
+    best = None
+    for kind in _lib.KERNEL_NAMES:
+        for lvl in range(L):
+            n, ms, b = mg.profile_get(kind, lvl)
+            if n and (best is None or ms > best[3]):
+                best = (kind, lvl, n, ms, b)
     mg.profile(False)
     mg.close()
 
     roof = None
-    if n0:
-        # algorithmic bytes per launch: 40 B per point per RB sweep
-        # x the sweeps one launch performs (temporal blocking fuses up to 3)
+    if best:
+        kind, lvl, n0, ms0, b0 = best
+        # algorithmic bytes per launch: 40 B/point per RB sweep,
+        # x the sweeps one launch performs, + the fused residual/restriction,
+        # prolongation+add or residual+norm it absorbs
         per_launch_bytes = b0 / n0
-        sweeps = per_launch_bytes / (GS_BYTES_PER_PT * (N + 1) ** 2)
         avg_s = ms0 * 1e-3 / n0
         achieved = per_launch_bytes / avg_s / 1e9
+        kname = KERNEL_IDS.get((kind, lvl)) if (N, L, args.nsmooth, args.smoother,
+                                                args.fuse) == (16384, 9, 3, 0, 3) else None
+        traffic = None
+        if kname:
+            prof = os.path.join(ROOT, "profiles", "r1_hbm_traffic.json")
+            if os.path.exists(prof):
+                t = json.load(open(prof))["kernels"].get(kname)
+                traffic = t["hbm_bytes"] if t else None
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": f"finest-level RB-GS pass ({sweeps:.0f} sweep(s) per launch)",
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": f"{_lib.KERNEL_NAMES[kind]} level {lvl}"
+                          + (f" = {kname}" if kname else ""),
                 "per_launch_bytes": per_launch_bytes, "avg_launch_ms": round(avg_s * 1e3, 4)}
+        if traffic:
+            # measured HBM bytes (rocprofv3 PMC, profiles/) / live mean duration
+            roof["hbm_GBs"] = round(traffic / avg_s / 1e9, 1)
+            roof["hbm_frac"] = round(traffic / avg_s / 1e9 / HBM_PEAK_GBS, 4)
 
     value = (N - 1) ** 2 * args.steps * world / elapsed
     out = {
