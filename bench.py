@@ -10,7 +10,13 @@ mg_outer computes after it (multigrid.cpp:112-113), with a fixed cycle count
 rotating velocity, nu=-4e-4, dt=dx/10) at N=16384, L=9 levels (coarsest 64),
 3 pre/post RB-GS sweeps, fp64; inputs resident in HBM before the timed region.
 
-value = (N-1)^2 * steps * ranks / max-over-ranks seconds.
+value = (N-1)^2 * steps / max-over-ranks seconds (whole job).
+Multi-GPU (torch.distributed.run, one rank per GPU): the north star's strong
+scaling -- the same N=16384 grid row-partitioned over the ranks (libmgx RCCL
+halo exchange, replicated coarse levels), "scaling":
+"strong".  --weak instead doubles N (and adds a level) per 4x ranks, so the
+points per GPU stay within 2x of the 1-GPU run, "scaling": "weak"
+(configs[4], N=65536 on 8 GPUs: --N 65536 --levels 11).
 roofline: the dominant kernel (largest device time: a finest-level fused
 smoothing pass) with achieved = its algorithmic bytes per launch (SURVEY 8d:
 40 B/point per RB sweep x 3 sweeps + the fused residual/restriction or
@@ -53,6 +59,9 @@ def parse():
     ap.add_argument("--cpu-baseline", choices=["auto", "off", "reference", "port"],
                     default="auto")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--weak", action="store_true",
+                    help="multi-GPU: grow N with the GPU count (N*2 per 4x GPUs) instead of "
+                         "partitioning the same grid")
     ap.add_argument("--no-profile", action="store_true",
                     help="do not record per-kernel HIP events in the timed region")
     return ap.parse_args()
@@ -112,11 +121,21 @@ def main():
             dist.barrier()
 
     N, L = args.N, args.levels
+    if args.weak and world > 1:
+        # points per GPU ~ constant: N grows by 2 per 4x ranks (power of two)
+        g = 1
+        while 4 * g <= world:
+            N, L, g = 2 * N, L + 1, 4 * g
     nu = -4e-4
     dt = 1.0 / N / 10
     u0, v1, v2 = pkg.init_problem(N, nthreads=16)
+    dist_kw = {}
+    if world > 1:
+        from hpcclassmultigridproject_amd import dist as mgdist
+        dist_kw = dict(world=world, rank=rank, unique_id=mgdist.broadcast_unique_id())
     mg = pkg.Multigrid(N, L, dt, nu, nsmooth=args.nsmooth, device=local,
-                       smoother=args.smoother, fuse=args.fuse)
+                       smoother=args.smoother, fuse=args.fuse, **dist_kw)
+    la = mg.dist_info()[2]
     mg.upload(u0, v1, v2)
     del u0, v1, v2
     mg.rhs()
@@ -190,19 +209,22 @@ def main():
             roof["hbm_GBs"] = round(traffic / avg_s / 1e9, 1)
             roof["hbm_frac"] = round(traffic / avg_s / 1e9 / HBM_PEAK_GBS, 4)
 
-    value = (N - 1) ** 2 * args.steps * world / elapsed
+    value = (N - 1) ** 2 * args.steps / elapsed
     out = {
         "metric": "V-cycle grid-point-updates/sec at N=16384; achieved HBM GB/s vs peak",
         "value": value, "unit": "grid-point-updates/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "scaling": "weak" if (args.weak or world == 1) else "strong",
+        "vs_baseline": None, "dtype": "f64",
         "data": "synthetic: the reference problem (Gaussian u0, rotating velocity), "
                 "generated on the host with glibc libm",
         "config": {"workload": f"N={N} fp64 V-cycle, L={L} (coarsest {N >> (L - 1)}), "
                                f"nu_smooth={args.nsmooth}, + residual/norm per step",
                    "N": N, "levels": L, "nsmooth": args.nsmooth,
-                   "parallelism": "replicas" if world > 1 else "single",
+                   "parallelism": (f"row-partition x{world} on levels 0..{la - 1}, "
+                                   f"levels {la}..{L - 1} replicated" if world > 1
+                                   else "single"),
                    "last_residual": res},
         "roofline": roof,
         "kernels": kernels,

@@ -15,6 +15,7 @@ HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "mgx.h")
 
 MGX_OK, MGX_E_ARG, MGX_E_HIP, MGX_E_RCCL, MGX_E_NOCONV = 0, 1, 2, 3, 4
 TOWER_REFERENCE, TOWER_CORRECT = 0, 1
+UNIQUE_ID_BYTES = 128   # MGX_UNIQUE_ID_BYTES (ncclUniqueId)
 K_GS, K_RESTRICT, K_PROLONG, K_RESNORM, K_COARSE, K_RHS, K_HALO, K_PSMOOTH = range(8)
 KERNEL_NAMES = {K_GS: "gs_sweep", K_RESTRICT: "residual_restrict", K_PROLONG: "prolong_add",
                 K_RESNORM: "residual_norm", K_COARSE: "coarse_solve", K_RHS: "compute_rhs",
@@ -77,6 +78,11 @@ _SIGS = {
     "mgx_profile_reset": (_I, [_vp]),
     "mgx_profile_get": (_I, [_vp, _I, _I, C.POINTER(_L), _dp, _dp]),
     "mgx_set_tuning": (_I, [C.c_char_p, _L]),
+    "mgx_dist_unique_id": (_I, [_vp]),
+    "mgx_create_dist": (_I, [C.POINTER(_vp), _L, _I, _D, _D, C.POINTER(Options), _I, _I, _vp]),
+    "mgx_create_local_dist": (_I, [C.POINTER(_vp), _L, _I, _D, _D, C.POINTER(Options), _I]),
+    "mgx_partition": (_I, [_L, _I, _I, _I, _I, C.POINTER(_I), C.POINTER(_I), C.POINTER(_I)]),
+    "mgx_dist_info": (_I, [_vp, C.POINTER(_I), C.POINTER(_I), C.POINTER(_I)]),
     "mgx_get_tuning": (_I, [C.c_char_p, C.POINTER(_L)]),
 }
 

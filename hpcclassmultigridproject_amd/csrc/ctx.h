@@ -1,0 +1,126 @@
+// ctx.h -- internal: the solver context shared by mgx.hip (single GPU) and
+// dist.hip (row-partitioned, multi-GPU).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/mgx.h"
+#include "kernels.h"
+
+namespace mgxi {
+
+int fail(int code, const std::string &msg);
+int check_launch(const char *what);
+
+#define HIPCHK(expr)                                                                     \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            return ::mgxi::fail(MGX_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+#define CHK(expr)              \
+    do {                       \
+        int rc_ = (expr);      \
+        if (rc_) return rc_;   \
+    } while (0)
+
+struct Level {
+    long n = 0, pitch = 0;
+    double *u[2] = {nullptr, nullptr};
+    int cur = 0;
+    bool zero = false;   // u is logically all zeros (multigrid.cpp:77), not yet written
+    double *rhs = nullptr, *v1 = nullptr, *v2 = nullptr;
+    mgx::Coef coef{};
+    double M() const { return double(n + 1) * double(n + 1); }
+    double *U() const { return u[cur]; }
+};
+
+struct ProfRec {
+    int kind, level;
+    double bytes;
+    hipEvent_t e0, e1;
+};
+
+struct Dist;   // dist.hip
+
+}  // namespace mgxi
+
+struct mgx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = true;
+    long N = 0;
+    int L = 0;
+    double dt = 0, nu = 0;
+    mgx_options opt{};
+    std::vector<mgxi::Level> lv;
+    double *partials = nullptr;   // norm partial sums
+    double *dscal = nullptr;      // [0] norm, [2..3] coarse stats (iterations, last norm)
+    double *hscal = nullptr;      // pinned host mirror
+    double *stage[2] = {nullptr, nullptr};   // reference-layout (N+1)^2 staging
+    mgxi::Dist *dist = nullptr;   // row-partitioned multi-GPU state (dist.hip)
+    // profiling
+    bool prof = false;
+    std::vector<mgxi::ProfRec> pending;
+    std::vector<hipEvent_t> pool;
+    double sum_ms[MGX_K_COUNT][64] = {};
+    double sum_bytes[MGX_K_COUNT][64] = {};
+    long count[MGX_K_COUNT][64] = {};
+};
+
+namespace mgxi {
+
+hipEvent_t take_event(mgx_ctx *c);
+
+// Launch helper: records HIP events around the launch when profiling is on.
+template <class F>
+int launch(mgx_ctx *c, int kind, int level, double bytes, F &&f) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (c->prof) {
+        e0 = take_event(c);
+        e1 = take_event(c);
+        if (e0) (void)hipEventRecord(e0, c->stream);
+    }
+    f();
+    CHK(check_launch("kernel launch"));
+    if (c->prof && e0 && e1) {
+        (void)hipEventRecord(e1, c->stream);
+        c->pending.push_back({kind, level, bytes, e0, e1});
+    }
+    return MGX_OK;
+}
+
+int prof_flush(mgx_ctx *c);
+int materialize(mgx_ctx *c, int l);
+int read_norm(mgx_ctx *c, double *norm);
+int op_vcycle(mgx_ctx *c, int l, double *norm = nullptr);
+int op_rhs(mgx_ctx *c);
+int op_residual_norm(mgx_ctx *c, int l, double *norm, double bytes_per_pt = 48.0);
+int build_tower(mgx_ctx *c);
+void free_ctx(mgx_ctx *c);
+// Create a single-GPU context; stream != nullptr: borrow that stream.
+int create_ctx(mgx_ctx **out, long n, int maxlvl, double dt, double nu, const mgx_options *opt,
+               hipStream_t stream);
+int upload_ctx(mgx_ctx *c, const double *u0, const double *v1, const double *v2,
+               hipMemcpyKind kind);
+
+// dist.hip entry points used by the C ABI
+int dist_upload(mgx_ctx *c, const double *u0, const double *v1, const double *v2,
+                hipMemcpyKind kind);
+int dist_download(mgx_ctx *c, double *u, hipMemcpyKind kind);
+int dist_rhs(mgx_ctx *c);
+int dist_vcycle(mgx_ctx *c, double *norm);
+int dist_residual_norm(mgx_ctx *c, double *norm);
+void dist_free(mgx_ctx *c);
+// replicated coarse-level contexts of a partitioned context (one per local part)
+int dist_nsub(mgx_ctx *c);
+mgx_ctx *dist_sub(mgx_ctx *c, int i);
+int dist_la(mgx_ctx *c);
+// levels whose row blocks would be shorter than this are replicated (tuning
+// key "dist_min_rows", default 256)
+extern long g_dist_min_rows;
+
+}  // namespace mgxi

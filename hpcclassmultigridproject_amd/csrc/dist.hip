@@ -1,0 +1,620 @@
+// dist.hip -- row-partitioned multi-GPU V-cycle.
+//
+// Levels 0..la-1 are split into contiguous row blocks, one per rank (even
+// block boundaries, so restriction rows 2I and prolongation parents stay
+// local).  Each block carries kGhost rows of its neighbours on each side;
+// because a fused smoothing pass of E stages is exact on the owned rows
+// given E ghost rows (the temporal-blocking cone, kernels.hip k_smooth), ONE
+// halo exchange per fused pass is enough -- where a sweep-by-sweep smoother
+// needs two per sweep.  Levels la..L-1 (where a block would be small) are
+// replicated: the restricted rhs is all-gathered into a full single-GPU
+// context on every rank, which runs the rest of the V-cycle redundantly and
+// bitwise identically, and the post-smoothing pass of level la-1 prolongs
+// from its (full) solution with no further exchange.  The residual norm of
+// the finest level is a per-rank partial sum + all-reduce.
+//
+// Two transports with the same partition logic:
+//   * RCCL (mgx_create_dist): one process per GPU, ncclSend/ncclRecv of whole
+//     ghost-row blocks (contiguous in the pitched layout) to rank +-1 over
+//     xGMI, ncclAllGather / ncclAllReduce, all on the context stream;
+//   * local (mgx_create_local_dist): `world` virtual ranks in one process on
+//     one device, exchanges as device-to-device copies -- for testing the
+//     partitioned solver against the single-GPU one on a one-GPU machine.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ctx.h"
+
+namespace mgxi {
+
+constexpr int kGhost = 8;            // >= the widest fused-pass cone (E <= 7) + 1
+long g_dist_min_rows = 256;
+
+#define NCCLCHK(expr)                                                                    \
+    do {                                                                                 \
+        ncclResult_t r_ = (expr);                                                        \
+        if (r_ != ncclSuccess)                                                           \
+            return fail(MGX_E_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+struct PLevel {
+    long n = 0, pitch = 0;
+    int ra = 0, rb = 0;   // owned rows [ra, rb)
+    int lo = 0, hi = 0;   // allocated rows [lo, hi] (owned + ghosts, clipped to [0, n])
+    double *u[2] = {nullptr, nullptr};
+    int cur = 0;
+    bool zero = false;
+    double *rhs = nullptr, *v1 = nullptr, *v2 = nullptr;
+    mgx::Coef coef{};
+    // field pointer offset so that F(a) + r*pitch is global row r
+    double *F(double *a) const { return a - (long)lo * pitch; }
+    double *U() const { return F(u[cur]); }
+    size_t bytes() const { return sizeof(double) * (size_t)(hi - lo + 1) * pitch; }
+    double Mown() const { return double(rb - ra) * double(n + 1); }
+};
+
+struct Part {
+    int rank = 0;
+    std::vector<PLevel> lv;   // levels 0..la-1
+    mgx_ctx *sub = nullptr;   // levels la..L-1, full, replicated
+    double *dsum = nullptr;   // device scalar: this rank's partial sum of squares
+};
+
+struct Dist {
+    int world = 1;
+    bool local = false;
+    int la = 0;
+    std::vector<Part> parts;   // local: `world` parts; RCCL: this rank's part
+    ncclComm_t comm = nullptr;
+    double *hsum = nullptr;    // pinned
+};
+
+// Partition plan: rows of level l owned by `rank` (same rule on every rank).
+static void plan_rows(long n0, int l, int world, int rank, int *ra, int *rb) {
+    const long nl = n0 >> l;
+    const long q = nl / world;
+    *ra = (int)(rank * q);
+    *rb = rank == world - 1 ? (int)nl + 1 : (int)((rank + 1) * q);
+}
+
+static int plan_la(long n0, int L, int world) {
+    if (world <= 1) return L - 1 > 0 ? L - 1 : 0;
+    int la = 0;
+    while (la < L - 1 && ((n0 >> la) / world) >= g_dist_min_rows) ++la;
+    return la;
+}
+
+void dist_free(mgx_ctx *c) {
+    Dist *d = c->dist;
+    if (!d) return;
+    for (auto &p : d->parts) {
+        for (auto &L : p.lv) {
+            (void)hipFree(L.u[0]);
+            (void)hipFree(L.u[1]);
+            (void)hipFree(L.rhs);
+            (void)hipFree(L.v1);
+            (void)hipFree(L.v2);
+        }
+        if (p.sub) free_ctx(p.sub);
+        (void)hipFree(p.dsum);
+    }
+    if (d->comm) (void)ncclCommDestroy(d->comm);
+    if (d->hsum) (void)hipHostFree(d->hsum);
+    delete d;
+    c->dist = nullptr;
+}
+
+static int build_dist(mgx_ctx *c, int world, const std::vector<int> &ranks) {
+    Dist *d = c->dist;
+    d->world = world;
+    d->la = plan_la(c->N, c->L, world);
+    HIPCHK(hipHostMalloc(&d->hsum, sizeof(double) * 8));
+    for (int r : ranks) {
+        Part p;
+        p.rank = r;
+        double h = 1.0 / c->N;
+        for (int l = 0; l < d->la; ++l) {
+            PLevel L;
+            L.n = c->N >> l;
+            L.pitch = mgx::tower_pitch(L.n);
+            L.coef = mgx::make_coef(c->dt, c->nu, h);
+            plan_rows(c->N, l, world, r, &L.ra, &L.rb);
+            L.lo = std::max(0, L.ra - kGhost);
+            L.hi = (int)std::min<long>(L.n, (long)L.rb - 1 + kGhost);
+            double **bufs[5] = {&L.u[0], &L.u[1], &L.rhs, &L.v1, &L.v2};
+            for (double **b : bufs) {
+                HIPCHK(hipMalloc(b, L.bytes()));
+                HIPCHK(hipMemsetAsync(*b, 0, L.bytes(), c->stream));
+            }
+            p.lv.push_back(L);
+            h = 2 * h;
+        }
+        mgx_options so = c->opt;
+        so.device = -1;
+        CHK(create_ctx(&p.sub, c->N >> d->la, c->L - d->la, c->dt, c->nu, &so, c->stream));
+        HIPCHK(hipMalloc(&p.dsum, sizeof(double) * 8));
+        d->parts.push_back(p);
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return MGX_OK;
+}
+
+// ---------------------------------------------------------------- transport
+enum Field { kU, kRhs };
+
+static double *field(const PLevel &L, Field f) { return f == kU ? L.U() : L.F(L.rhs); }
+
+// Refresh the ghost rows of `f` on level l from the neighbouring ranks.
+static int exchange_rows(mgx_ctx *c, int l, Field f) {
+    Dist *d = c->dist;
+    if (d->local) {
+        for (size_t i = 0; i < d->parts.size(); ++i) {
+            PLevel &L = d->parts[i].lv[l];
+            const long P = L.pitch;
+            double *dst = field(L, f);
+            if (i > 0) {   // rows [lo, ra) from rank i-1
+                const PLevel &A = d->parts[i - 1].lv[l];
+                HIPCHK(hipMemcpyAsync(dst + (long)L.lo * P, field(A, f) + (long)L.lo * P,
+                                      sizeof(double) * (L.ra - L.lo) * P,
+                                      hipMemcpyDeviceToDevice, c->stream));
+            }
+            if (i + 1 < d->parts.size()) {   // rows [rb, hi] from rank i+1
+                const PLevel &B = d->parts[i + 1].lv[l];
+                HIPCHK(hipMemcpyAsync(dst + (long)L.rb * P, field(B, f) + (long)L.rb * P,
+                                      sizeof(double) * (L.hi - L.rb + 1) * P,
+                                      hipMemcpyDeviceToDevice, c->stream));
+            }
+        }
+        return MGX_OK;
+    }
+    Part &p = d->parts[0];
+    PLevel &L = p.lv[l];
+    const long P = L.pitch;
+    double *a = field(L, f);
+    NCCLCHK(ncclGroupStart());
+    if (p.rank > 0) {
+        const size_t cnt = (size_t)(L.ra - L.lo) * P;
+        NCCLCHK(ncclSend(a + (long)L.ra * P, cnt, ncclDouble, p.rank - 1, d->comm, c->stream));
+        NCCLCHK(ncclRecv(a + (long)L.lo * P, cnt, ncclDouble, p.rank - 1, d->comm, c->stream));
+    }
+    if (p.rank < d->world - 1) {
+        const int g = L.hi - L.rb + 1;
+        const size_t cnt = (size_t)g * P;
+        NCCLCHK(ncclSend(a + (long)(L.rb - g) * P, cnt, ncclDouble, p.rank + 1, d->comm,
+                         c->stream));
+        NCCLCHK(ncclRecv(a + (long)L.rb * P, cnt, ncclDouble, p.rank + 1, d->comm, c->stream));
+    }
+    NCCLCHK(ncclGroupEnd());
+    return MGX_OK;
+}
+
+static int exchange(mgx_ctx *c, int l, Field f) {
+    if (c->dist->world == 1) return MGX_OK;
+    int rc = MGX_OK;
+    const PLevel &L = c->dist->parts[0].lv[l];
+    const double bytes = 16.0 * kGhost * L.pitch * c->dist->parts.size();
+    CHK(launch(c, MGX_K_HALO, l, bytes, [&] { rc = exchange_rows(c, l, f); }));
+    return rc;
+}
+
+// Restricted rhs of the first replicated level: every rank wrote its own rows
+// of the full array in its sub-context; make them whole everywhere.
+static int gather_rhs(mgx_ctx *c) {
+    Dist *d = c->dist;
+    const long nl = c->N >> d->la;
+    const long q = nl / d->world;   // rows per rank; row nl (boundary) is never read
+    if (d->world > 1) {
+        if (d->local) {
+            for (auto &dst : d->parts)
+                for (auto &src : d->parts) {
+                    if (&dst == &src) continue;
+                    const long P = dst.sub->lv[0].pitch, off = (long)src.rank * q * P;
+                    HIPCHK(hipMemcpyAsync(dst.sub->lv[0].rhs + off, src.sub->lv[0].rhs + off,
+                                          sizeof(double) * q * P, hipMemcpyDeviceToDevice,
+                                          c->stream));
+                }
+        } else {
+            Part &p = d->parts[0];
+            const long P = p.sub->lv[0].pitch;
+            double *rhs = p.sub->lv[0].rhs;
+            NCCLCHK(ncclAllGather(rhs + (long)p.rank * q * P, rhs, (size_t)q * P, ncclDouble,
+                                  d->comm, c->stream));
+        }
+    }
+    for (auto &p : d->parts) p.sub->lv[0].zero = true;   // u[la] = 0 (multigrid.cpp:77)
+    return MGX_OK;
+}
+
+// Sum the ranks' partial sums of squares -> norm on the host.
+static int reduce_norm(mgx_ctx *c, double *norm) {
+    Dist *d = c->dist;
+    double tot = 0.0;
+    if (d->local) {
+        for (auto &p : d->parts) {
+            HIPCHK(hipMemcpyAsync(d->hsum, p.dsum, sizeof(double), hipMemcpyDeviceToHost,
+                                  c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            tot += d->hsum[0];
+        }
+    } else {
+        Part &p = d->parts[0];
+        NCCLCHK(ncclAllReduce(p.dsum, p.dsum, 1, ncclDouble, ncclSum, d->comm, c->stream));
+        HIPCHK(hipMemcpyAsync(d->hsum, p.dsum, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        tot = d->hsum[0];
+    }
+    *norm = std::sqrt(tot);
+    return MGX_OK;
+}
+
+// ---------------------------------------------------------------- V-cycle
+static mgx::SmoothArgs args_for(const PLevel &L) {
+    mgx::SmoothArgs A{};
+    A.uin = L.U();
+    A.uout = L.F(L.u[L.cur ^ 1]);
+    A.rhs = L.F(L.rhs);
+    A.v1 = L.F(L.v1);
+    A.v2 = L.F(L.v2);
+    A.n = L.n;
+    A.pitch = L.pitch;
+    A.c = L.coef;
+    A.ra = L.ra;
+    A.rb = L.rb;
+    A.lo = L.lo;
+    A.hi = L.hi;
+    return A;
+}
+
+// nsmooth sweeps on partitioned level l in passes of <= fuse sweeps; the
+// first pass may add the prolongation, the last may restrict or take the norm.
+static int smooth(mgx_ctx *c, int l, bool prolong, bool restrict_, bool norm) {
+    Dist *d = c->dist;
+    const int sweeps = c->opt.nsmooth;
+    const int fuse = std::max(1, std::min(c->opt.fuse, mgx::kSmoothMaxSweeps));
+    for (int done = 0; done < sweeps;) {
+        const int k = std::min(sweeps - done, fuse);
+        const bool first = done == 0, last = done + k == sweeps;
+        const bool zero = d->parts[0].lv[l].zero;
+        const bool pr = prolong && first && !zero;
+        const bool rs = restrict_ && last;
+        const bool nm = norm && last && !rs;
+        if (!zero) CHK(exchange(c, l, kU));
+        if (pr && l + 1 < d->la) CHK(exchange(c, l + 1, kU));
+        int mode = 0;
+        if (zero) mode |= mgx::kModeZero;
+        if (pr) mode |= mgx::kModeProlong;
+        if (rs) mode |= mgx::kModeRestrict;
+        if (nm) mode |= mgx::kModeNorm;
+        for (auto &p : d->parts) {
+            PLevel &L = p.lv[l];
+            mgx::SmoothArgs A = args_for(L);
+            if (pr || rs) {
+                if (l + 1 < d->la) {
+                    PLevel &Cl = p.lv[l + 1];
+                    A.uc = Cl.U();
+                    A.rhsc = Cl.F(Cl.rhs);
+                    A.pitchc = Cl.pitch;
+                } else {
+                    Level &Cl = p.sub->lv[0];
+                    A.uc = Cl.U();
+                    A.rhsc = Cl.rhs;
+                    A.pitchc = Cl.pitch;
+                }
+            }
+            A.partials = c->partials;
+            A.norm_out = p.dsum;
+            A.norm_sqrt = false;
+            double bytes = 40.0 * k * L.Mown();
+            int blocks = 0;
+            CHK(launch(c, pr ? MGX_K_PSMOOTH : MGX_K_GS, l, bytes,
+                       [&] { blocks = mgx::launch_smooth(A, k, mode, c->stream); }));
+            if (blocks < 0) return fail(MGX_E_ARG, "launch_smooth: unsupported sweeps/mode");
+            L.cur ^= 1;
+            L.zero = false;
+        }
+        done += k;
+    }
+    return MGX_OK;
+}
+
+static int dist_level(mgx_ctx *c, int l, bool want_norm) {
+    Dist *d = c->dist;
+    for (int sh = 0; sh < c->opt.shape; ++sh) {
+        const bool last = sh == c->opt.shape - 1;
+        CHK(smooth(c, l, false, /*restrict=*/true, false));
+        if (l + 1 < d->la) {
+            CHK(exchange(c, l + 1, kRhs));
+            for (auto &p : d->parts) p.lv[l + 1].zero = true;
+            CHK(dist_level(c, l + 1, false));
+        } else {
+            CHK(gather_rhs(c));
+            for (auto &p : d->parts) CHK(op_vcycle(p.sub, 0));
+        }
+        CHK(smooth(c, l, /*prolong=*/true, false, want_norm && last));
+    }
+    return MGX_OK;
+}
+
+int dist_vcycle(mgx_ctx *c, double *norm) {
+    Dist *d = c->dist;
+    if (d->la == 0) {   // everything replicated
+        for (auto &p : d->parts) CHK(op_vcycle(p.sub, 0, norm));
+        return MGX_OK;
+    }
+    CHK(dist_level(c, 0, norm != nullptr));
+    if (norm) CHK(reduce_norm(c, norm));
+    return MGX_OK;
+}
+
+int dist_residual_norm(mgx_ctx *c, double *norm) {
+    Dist *d = c->dist;
+    if (d->la == 0) {
+        for (auto &p : d->parts) CHK(op_residual_norm(p.sub, 0, norm));
+        return MGX_OK;
+    }
+    CHK(exchange(c, 0, kU));
+    for (auto &p : d->parts) {
+        PLevel &L = p.lv[0];
+        CHK(launch(c, MGX_K_RESNORM, 0, 48.0 * L.Mown(), [&] {
+            mgx::launch_residual_norm(L.U(), L.F(L.rhs), L.F(L.v1), L.F(L.v2), L.n, L.pitch,
+                                      L.coef, c->partials, p.dsum, c->stream, L.ra, L.rb,
+                                      /*take_sqrt=*/false);
+        }));
+    }
+    return reduce_norm(c, norm);
+}
+
+int dist_rhs(mgx_ctx *c) {
+    Dist *d = c->dist;
+    if (d->la == 0) {
+        for (auto &p : d->parts) CHK(op_rhs(p.sub));
+        return MGX_OK;
+    }
+    CHK(exchange(c, 0, kU));
+    for (auto &p : d->parts) {
+        PLevel &L = p.lv[0];
+        CHK(launch(c, MGX_K_RHS, 0, 32.0 * L.Mown(), [&] {
+            mgx::launch_rhs(L.F(L.rhs), L.U(), L.F(L.v1), L.F(L.v2), L.n, L.pitch, L.coef,
+                            c->stream, L.ra, L.rb);
+        }));
+    }
+    return exchange(c, 0, kRhs);
+}
+
+int dist_nsub(mgx_ctx *c) { return c->dist ? (int)c->dist->parts.size() : 0; }
+mgx_ctx *dist_sub(mgx_ctx *c, int i) { return c->dist->parts[i].sub; }
+int dist_la(mgx_ctx *c) { return c->dist ? c->dist->la : c->L; }
+
+// ---------------------------------------------------------------- data movement
+// Build the full tower in a temporary single-GPU context (the reference
+// construction, multigrid.cpp:148-160), then copy every rank's rows out of it.
+int dist_upload(mgx_ctx *c, const double *u0, const double *v1, const double *v2,
+                hipMemcpyKind kind) {
+    Dist *d = c->dist;
+    mgx_options o = c->opt;
+    o.device = -1;
+    mgx_ctx *T = nullptr;
+    CHK(create_ctx(&T, c->N, c->L, c->dt, c->nu, &o, c->stream));
+    int rc = upload_ctx(T, u0, v1, v2, kind);
+    for (auto &p : d->parts) {
+        for (int l = 0; rc == MGX_OK && l < d->la; ++l) {
+            PLevel &L = p.lv[l];
+            Level &F = T->lv[l];
+            const size_t cnt = sizeof(double) * (size_t)(L.hi - L.lo + 1) * L.pitch;
+            const long off = (long)L.lo * L.pitch;
+            rc = hipMemcpyAsync(L.v1, F.v1 + off, cnt, hipMemcpyDeviceToDevice, c->stream) ||
+                 hipMemcpyAsync(L.v2, F.v2 + off, cnt, hipMemcpyDeviceToDevice, c->stream);
+            if (rc == MGX_OK && l == 0)
+                rc = hipMemcpyAsync(L.u[0], F.U() + off, cnt, hipMemcpyDeviceToDevice, c->stream);
+            if (rc == MGX_OK)
+                rc = hipMemsetAsync(L.rhs, 0, cnt, c->stream) ||
+                     (l > 0 ? hipMemsetAsync(L.u[0], 0, cnt, c->stream) : hipSuccess);
+            if (rc) rc = fail(MGX_E_HIP, "dist_upload: copy");
+            L.cur = 0;
+            L.zero = false;
+        }
+        for (int l = d->la; rc == MGX_OK && l < c->L; ++l) {
+            Level &S = p.sub->lv[l - d->la];
+            Level &F = T->lv[l];
+            const size_t cnt = sizeof(double) * (size_t)(F.n + 1) * F.pitch;
+            rc = hipMemcpyAsync(S.v1, F.v1, cnt, hipMemcpyDeviceToDevice, c->stream) ||
+                 hipMemcpyAsync(S.v2, F.v2, cnt, hipMemcpyDeviceToDevice, c->stream);
+            if (rc == MGX_OK && l == 0)
+                rc = hipMemcpyAsync(S.u[0], F.U(), cnt, hipMemcpyDeviceToDevice, c->stream);
+            if (rc) rc = fail(MGX_E_HIP, "dist_upload: copy");
+            S.cur = 0;
+            S.zero = false;
+        }
+    }
+    if (rc == MGX_OK && hipStreamSynchronize(c->stream) != hipSuccess)
+        rc = fail(MGX_E_HIP, "dist_upload: sync");
+    free_ctx(T);
+    return rc;
+}
+
+int dist_download(mgx_ctx *c, double *u, hipMemcpyKind kind) {
+    Dist *d = c->dist;
+    if (d->la == 0) {
+        mgx_ctx *s = d->parts[0].sub;
+        Level &L = s->lv[0];
+        const size_t row = (L.n + 1) * sizeof(double);
+        HIPCHK(hipMemcpy2DAsync(u, row, L.U(), L.pitch * sizeof(double), row, L.n + 1, kind,
+                                c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return MGX_OK;
+    }
+    const long n = c->N;
+    const size_t row = (n + 1) * sizeof(double);
+    if (d->local) {
+        for (auto &p : d->parts) {
+            PLevel &L = p.lv[0];
+            HIPCHK(hipMemcpy2DAsync(u + (long)L.ra * (n + 1), row, L.U() + (long)L.ra * L.pitch,
+                                    L.pitch * sizeof(double), row, L.rb - L.ra, kind, c->stream));
+        }
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return MGX_OK;
+    }
+    // RCCL: all-gather the owned blocks into a full temporary, then copy out
+    Part &p = d->parts[0];
+    PLevel &L = p.lv[0];
+    const long P = L.pitch, q = n / d->world;
+    double *full = nullptr;
+    HIPCHK(hipMalloc(&full, sizeof(double) * (size_t)(n + 1) * P));
+    int rc = MGX_OK;
+    ncclResult_t r1 = ncclAllGather(L.U() + (long)L.ra * P, full, (size_t)q * P, ncclDouble,
+                                    d->comm, c->stream);
+    // Drain before the next enqueue: with a size-1 communicator, RCCL 2.27's
+    // all-gather followed directly by further stream work segfaulted on the
+    // host (tests/test_gpu_dist.py::test_rccl_world1_equals_single).  The
+    // download is off the hot path, so the sync costs nothing that matters.
+    if (r1 == ncclSuccess && hipStreamSynchronize(c->stream) != hipSuccess) {
+        (void)hipFree(full);
+        return fail(MGX_E_HIP, "dist_download: sync");
+    }
+    // row n (boundary) lives on the last rank
+    if (r1 == ncclSuccess && p.rank == d->world - 1)
+        (void)hipMemcpyAsync(full + n * P, L.U() + n * P, sizeof(double) * P,
+                             hipMemcpyDeviceToDevice, c->stream);
+    if (r1 == ncclSuccess)
+        r1 = ncclBroadcast(full + n * P, full + n * P, (size_t)P, ncclDouble, d->world - 1,
+                           d->comm, c->stream);
+    if (r1 != ncclSuccess) rc = fail(MGX_E_RCCL, ncclGetErrorString(r1));
+    if (rc == MGX_OK &&
+        (hipMemcpy2DAsync(u, row, full, P * sizeof(double), row, n + 1, kind, c->stream) ||
+         hipStreamSynchronize(c->stream)))
+        rc = fail(MGX_E_HIP, "dist_download");
+    (void)hipFree(full);
+    return rc;
+}
+
+static int create_dist_common(mgx_ctx **out, long n, int maxlvl, double dt, double nu,
+                              const mgx_options *opt, mgx_ctx **cp) {
+    mgx_options o;
+    mgx_default_options(&o);
+    if (opt) o = *opt;
+    if (o.smoother != 0 || o.nsmooth < 1)
+        return fail(MGX_E_ARG, "partitioned contexts need smoother 0 and nsmooth >= 1");
+    // parent context: stream, scratch and options only; its level arrays are
+    // the parts' blocks (a 2x2 placeholder level is created and dropped)
+    mgx_ctx *c = nullptr;
+    CHK(create_ctx(&c, 2, 1, dt, nu, &o, nullptr));
+    for (auto &L : c->lv) {
+        (void)hipFree(L.u[0]);
+        (void)hipFree(L.u[1]);
+        (void)hipFree(L.rhs);
+        (void)hipFree(L.v1);
+        (void)hipFree(L.v2);
+    }
+    c->lv.clear();
+    c->N = n;
+    c->L = maxlvl;
+    c->dist = new Dist();
+    *cp = c;
+    (void)out;
+    return MGX_OK;
+}
+
+}  // namespace mgxi
+
+using namespace mgxi;
+
+extern "C" {
+
+int mgx_partition(long n, int maxlvl, int world, int rank, int level, int *ra, int *rb,
+                  int *replicated_level) {
+    if (n < 2 || maxlvl < 1 || world < 1 || rank < 0 || rank >= world || level < 0 ||
+        level >= maxlvl)
+        return fail(MGX_E_ARG, "mgx_partition: bad args");
+    const int la = plan_la(n, maxlvl, world);
+    if (replicated_level) *replicated_level = la;
+    if (level >= la) {   // replicated: every rank holds all rows
+        if (ra) *ra = 0;
+        if (rb) *rb = (int)(n >> level) + 1;
+    } else {
+        int a, b;
+        plan_rows(n, level, world, rank, &a, &b);
+        if (ra) *ra = a;
+        if (rb) *rb = b;
+    }
+    return MGX_OK;
+}
+
+int mgx_dist_unique_id(void *id128) {
+    if (!id128) return fail(MGX_E_ARG, "null id");
+    ncclUniqueId id;
+    NCCLCHK(ncclGetUniqueId(&id));
+    memcpy(id128, &id, sizeof(id));
+    return MGX_OK;
+}
+
+static int check_world(long n, int maxlvl, int world) {
+    if (world < 1 || (world & (world - 1)))
+        return fail(MGX_E_ARG, "world size must be a power of two");
+    if (maxlvl < 1 || (n >> (maxlvl - 1)) < 2) return fail(MGX_E_ARG, "bad maxlvl");
+    if (world > 1 && n / world < 2 * kGhost) return fail(MGX_E_ARG, "too many ranks for n");
+    return MGX_OK;
+}
+
+int mgx_create_dist(mgx_ctx **out, long n, int maxlvl, double dt, double nu,
+                    const mgx_options *opt, int rank, int world, const void *id128) {
+    if (!out || !id128 || rank < 0 || rank >= world) return fail(MGX_E_ARG, "mgx_create_dist: bad args");
+    *out = nullptr;
+    CHK(check_world(n, maxlvl, world));
+    if (n < 2 || (n & (n - 1))) return fail(MGX_E_ARG, "n must be a power of two");
+    mgx_ctx *c = nullptr;
+    CHK(create_dist_common(out, n, maxlvl, dt, nu, opt, &c));
+    c->dist->local = false;
+    {   // also for world == 1, so the download/norm collectives take one path
+        ncclUniqueId id;
+        memcpy(&id, id128, sizeof(id));
+        ncclResult_t r = ncclCommInitRank(&c->dist->comm, world, id, rank);
+        if (r != ncclSuccess) {
+            free_ctx(c);
+            return fail(MGX_E_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+        }
+    }
+    int rc = build_dist(c, world, {rank});
+    if (rc) {
+        free_ctx(c);
+        return rc;
+    }
+    *out = c;
+    return MGX_OK;
+}
+
+int mgx_create_local_dist(mgx_ctx **out, long n, int maxlvl, double dt, double nu,
+                          const mgx_options *opt, int world) {
+    if (!out) return fail(MGX_E_ARG, "mgx_create_local_dist: null out");
+    *out = nullptr;
+    CHK(check_world(n, maxlvl, world));
+    if (n < 2 || (n & (n - 1))) return fail(MGX_E_ARG, "n must be a power of two");
+    mgx_ctx *c = nullptr;
+    CHK(create_dist_common(out, n, maxlvl, dt, nu, opt, &c));
+    c->dist->local = true;
+    std::vector<int> ranks;
+    for (int r = 0; r < world; ++r) ranks.push_back(r);
+    int rc = build_dist(c, world, ranks);
+    if (rc) {
+        free_ctx(c);
+        return rc;
+    }
+    *out = c;
+    return MGX_OK;
+}
+
+int mgx_dist_info(mgx_ctx *c, int *world, int *rank, int *replicated_level) {
+    if (!c) return fail(MGX_E_ARG, "null ctx");
+    Dist *d = c->dist;
+    if (world) *world = d ? d->world : 1;
+    if (rank) *rank = d ? (d->local ? -1 : d->parts[0].rank) : 0;
+    if (replicated_level) *replicated_level = d ? d->la : c->L;
+    return MGX_OK;
+}
+
+}  // extern "C"

@@ -65,7 +65,13 @@ struct SmoothArgs {
     double *rhsc;       // coarse rhs (RESTRICT)
     long pitchc;        // pitch of the coarse level
     double *partials;   // NORM
-    double *norm_out;   // NORM
+    double *norm_out;   // NORM: sqrt of the sum (norm_sqrt) or the plain sum
+    bool norm_sqrt = true;
+    // Row-block partitions (multi-GPU): output rows [ra, rb) and rows [lo, hi]
+    // that hold valid data (owned + ghost rows), all global row indices; the
+    // field pointers are offset so that ptr + r*pitch is global row r.
+    // rb < 0 means the whole level: ra = 0, rb = n+1, lo = 0, hi = n.
+    int ra = 0, rb = -1, lo = 0, hi = -1;
 };
 int launch_smooth(const SmoothArgs &a, int sweeps, int mode, hipStream_t s);
 // Levels with n <= tile_max_n use the 2-D tile form of the fused pass (small
@@ -86,9 +92,11 @@ void launch_residual_restrict(const double *u, const double *rhs, const double *
                               const double *v2, long n, long pitch, Coef c, double *rhsc,
                               long pitchc, hipStream_t s);
 // residual + sum of squares (not stored): partial sums -> norm into *out.
+// Rows restricted to [ra, rb) (default: all); take_sqrt = false stores the sum.
 void launch_residual_norm(const double *u, const double *rhs, const double *v1,
                           const double *v2, long n, long pitch, Coef c, double *partials,
-                          double *out, hipStream_t s);
+                          double *out, hipStream_t s, int ra = 0, int rb = -1,
+                          bool take_sqrt = true);
 // residual stored (interior) into res (tower layout).
 void launch_residual(double *res, const double *u, const double *rhs, const double *v1,
                      const double *v2, long n, long pitch, Coef c, hipStream_t s);
@@ -96,7 +104,7 @@ void launch_residual(double *res, const double *u, const double *rhs, const doub
 void launch_prolong_add(double *uf, long pitchf, const double *uc, long pitchc, long nc,
                         hipStream_t s);
 void launch_rhs(double *rhs, const double *u, const double *v1, const double *v2, long n,
-                long pitch, Coef c, hipStream_t s);
+                long pitch, Coef c, hipStream_t s, int ra = 0, int rb = -1);
 // Coarsest-level solve in one workgroup: repeat {GS; residual; norm} while
 // norm > tol and it < maxit (multigrid.cpp:58-65), in place on u.
 // zero_first: u = 0 before the first sweep.  stats[0] += iterations,

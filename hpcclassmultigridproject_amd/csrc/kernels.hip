@@ -93,12 +93,13 @@ constexpr int kNormBlocks = 8192;   // capacity of the partials buffer
 constexpr int kFinalThreads = 1024;
 
 __global__ __launch_bounds__(kFinalThreads) void k_norm_final(const double *partials,
-                                                              int count, double *out) {
+                                                              int count, double *out,
+                                                              int take_sqrt = 1) {
     __shared__ double lds[16];
     double acc = 0.0;
     for (int i = threadIdx.x; i < count; i += kFinalThreads) acc += partials[i];
     double tot = block_sum(acc, lds);
-    if (threadIdx.x == 0) out[0] = sqrt(tot);
+    if (threadIdx.x == 0) out[0] = take_sqrt ? sqrt(tot) : tot;
 }
 
 // ============================================================ reference layout
@@ -439,7 +440,7 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
     const double *__restrict__ uin, double *__restrict__ uout, const double *__restrict__ rhs,
     const double *__restrict__ v1, const double *__restrict__ v2, const double *__restrict__ uc,
     long pitchc, double *__restrict__ rhsc, double *__restrict__ partials, int n, long pitch,
-    int strips, long units_per_wg, Coef c) {
+    int strips, long units_per_wg, Coef c, int ra, int rb, int lo, int hi) {
     using C = SmoothCfg<K, MODE>;
     constexpr int S = C::S, E = C::E, H = C::H, NR = C::NR, NS = C::NS;
     constexpr int LW = 2 * BLOCK + 2;   // LDS row: x = 1 + 2*lane + cs
@@ -447,16 +448,17 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
     __shared__ __attribute__((aligned(16))) double ring[NR][LW];
 
     const int l = threadIdx.x;
-    const long total = (long)strips * (n + 1);
+    const int nrows = rb - ra;
+    const long total = (long)strips * nrows;
     long start = (long)blockIdx.x * units_per_wg;
     const long end = min(total, start + units_per_wg);
     const int nc = n >> 1;
     double acc = 0.0;   // NORM partial
 
     while (start < end) {
-        const int strip = (int)(start / (n + 1));
-        const int a = (int)(start % (n + 1));
-        const int b = (int)min((long)(n + 1), (long)a + (end - start));
+        const int strip = (int)(start / nrows);
+        const int a = ra + (int)(start % nrows);
+        const int b = (int)min((long)rb, (long)a + (end - start));
         start += b - a;
 
         const int j0 = strip * W;
@@ -486,7 +488,7 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
         const int j1 = (jl + 1 <= nc) ? 1 : 0;
         auto load_u = [&](int R, UPre &u) {
             if (C::ZERO) return;
-            const int Rc = min(max(R, 0), n);
+            const int Rc = min(max(R, lo), hi);
             u.X = ld2((uin + (long)Rc * pitch) + cl);
             if (C::PROL) {
                 // branch-free: even rows read coarse row R/2 twice (cache hits)
@@ -518,7 +520,7 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
             st2(&ring[sl][x0], v);
         };
         auto load_rv = [&](int R, RowData &d) {
-            const long o = (long)min(max(R, 0), n) * pitch;   // scalar row offset
+            const long o = (long)min(max(R, lo), hi) * pitch;   // scalar row offset
             d.r = ld2((rhs + o) + cl);
             d.x = ld2((v1 + o) + cl);
             d.y = ld2((v2 + o) + cl);
@@ -663,7 +665,7 @@ __global__ __launch_bounds__(256) void k_smooth_tile(
     const double *__restrict__ uin, double *__restrict__ uout, const double *__restrict__ rhs,
     const double *__restrict__ v1, const double *__restrict__ v2, const double *__restrict__ uc,
     long pitchc, double *__restrict__ rhsc, double *__restrict__ partials, int n, long pitch,
-    int tiles_x, Coef c) {
+    int tiles_x, Coef c, int ra, int rb, int lo, int hi) {
     using C = SmoothCfg<K, MODE>;
     using T = TileCfg<K, MODE>;
     constexpr int S = C::S, EH = T::EH, WT = T::WT, PPT = T::PPT, HW = WT / 2;
@@ -671,7 +673,7 @@ __global__ __launch_bounds__(256) void k_smooth_tile(
 
     const int t = threadIdx.x;
     const int ty = blockIdx.x / tiles_x, tx = blockIdx.x % tiles_x;
-    const long i0 = (long)ty * T::TR - EH, j0 = (long)tx * T::TC - EH;   // tile origin (even)
+    const long i0 = ra + (long)ty * T::TR - EH, j0 = (long)tx * T::TC - EH;   // tile origin (even)
     const int nc = n >> 1;
 
     // rhs / v1 / v2 of the lane's pairs as scalar arrays (static indices only,
@@ -687,7 +689,7 @@ __global__ __launch_bounds__(256) void k_smooth_tile(
         const int r = q / HW, k = q % HW;
         const long gi = i0 + r, gj = j0 + 2 * k;
         double2 v = make_double2(0.0, 0.0);
-        if (gi >= 0 && gi <= n && gj >= 0 && gj <= n) {
+        if (gi >= lo && gi <= hi && gj >= 0 && gj <= n) {
             ok[m] = true;
             const long o = gi * pitch + gj;
             if (!C::ZERO) v = ld2(uin + o);
@@ -747,6 +749,7 @@ __global__ __launch_bounds__(256) void k_smooth_tile(
         const int r = q / HW, k = q % HW;
         if (r < EH || r >= EH + T::TR || 2 * k < EH || 2 * k >= EH + T::TC) continue;
         const long gi = i0 + r, gj = j0 + 2 * k;
+        if (gi >= rb) continue;
         const int x = r * WT + 2 * k;
         st2(uout + gi * pitch + gj, ld2(&tu[x]));
         if (C::REST || C::NORM) {
@@ -802,13 +805,15 @@ __global__ __launch_bounds__(256) void k_res_march(const double *__restrict__ u,
                                                    const double *__restrict__ v2, int n,
                                                    long pitch, Coef c, int rows_per_group,
                                                    double *__restrict__ out,
-                                                   double *__restrict__ partials) {
+                                                   double *__restrict__ partials, int r_first,
+                                                   int r_end) {
     __shared__ double lds[4];
     const int t = threadIdx.x, lane = t & 63;
     const long c0 = (long)blockIdx.x * 512 + 2 * t;
     const bool act = c0 <= n;
-    const long i0 = 1 + (long)blockIdx.y * rows_per_group;
-    const long i1 = std::min<long>(n, i0 + rows_per_group);
+    // interior rows [r_first, r_end) (a partition's owned rows, or 1..n-1)
+    const long i0 = r_first + (long)blockIdx.y * rows_per_group;
+    const long i1 = std::min<long>(r_end, i0 + rows_per_group);
     double acc = 0.0;
     const double2 z2 = make_double2(0.0, 0.0);
     double2 un = z2, um = z2, us = z2;
@@ -1071,7 +1076,7 @@ static int smooth_inst(const SmoothArgs &A, hipStream_t s) {
     }
     const long n = A.n;
     const int strips = (int)((n + 1 + W - 1) / W);
-    const long total = (long)strips * (n + 1);
+    const long total = (long)strips * (A.rb - A.ra);
     // at least ~64 rows per workgroup so the priming rows stay cheap; NORM
     // partials are bounded by the partials buffer
     long g = std::max<long>(1, std::min<long>(slots, total / 64));
@@ -1079,7 +1084,8 @@ static int smooth_inst(const SmoothArgs &A, hipStream_t s) {
     const long upw = (total + g - 1) / g;
     const unsigned grid = (unsigned)((total + upw - 1) / upw);
     MGX_LAUNCH((k_smooth<BLOCK, K, MODE>), dim3(grid), dim3(BLOCK), s, A.uin, A.uout, A.rhs, A.v1,
-               A.v2, A.uc, A.pitchc, A.rhsc, A.partials, (int)n, A.pitch, strips, upw, A.c);
+               A.v2, A.uc, A.pitchc, A.rhsc, A.partials, (int)n, A.pitch, strips, upw, A.c, A.ra,
+               A.rb, A.lo, A.hi);
     return (int)grid;
 }
 
@@ -1103,12 +1109,12 @@ static int smooth_tile_inst(const SmoothArgs &A, hipStream_t s) {
     using T = TileCfg<K, MODE>;
     const long n = A.n;
     const int tiles_x = (int)((n + 1 + T::TC - 1) / T::TC);
-    const int tiles_y = (int)((n + 1 + T::TR - 1) / T::TR);
+    const int tiles_y = (int)((A.rb - A.ra + T::TR - 1) / T::TR);
     const long grid = (long)tiles_x * tiles_y;
     if ((MODE & 8) && grid > kNormBlocks) return -1;
     MGX_LAUNCH((k_smooth_tile<K, MODE>), dim3((unsigned)grid), dim3(256), s, A.uin, A.uout,
                A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, A.partials, (int)n, A.pitch, tiles_x,
-               A.c);
+               A.c, A.ra, A.rb, A.lo, A.hi);
     return (int)grid;
 }
 
@@ -1152,7 +1158,15 @@ static int smooth_k(const SmoothArgs &A, int mode, hipStream_t s) {
     }
 }
 
-int launch_smooth(const SmoothArgs &A, int sweeps, int mode, hipStream_t s) {
+int launch_smooth(const SmoothArgs &A0, int sweeps, int mode, hipStream_t s) {
+    SmoothArgs A = A0;
+    if (A.rb < 0) {
+        A.ra = 0;
+        A.rb = (int)A.n + 1;
+        A.lo = 0;
+        A.hi = (int)A.n;
+    }
+    if (A.ra & 1) return -1;   // partitions start at even rows (parity, restriction)
     int blocks = -1;
     switch (sweeps) {
         case 1: blocks = smooth_k<1>(A, mode, s); break;
@@ -1162,7 +1176,7 @@ int launch_smooth(const SmoothArgs &A, int sweeps, int mode, hipStream_t s) {
     }
     if (blocks > 0 && (mode & 8))
         MGX_LAUNCH(k_norm_final, dim3(1), dim3(kFinalThreads), s, (const double *)A.partials,
-                   blocks, A.norm_out);
+                   blocks, A.norm_out, A.norm_sqrt ? 1 : 0);
     return blocks;
 }
 
@@ -1174,42 +1188,57 @@ void launch_gs_colour(double *u, const double *rhs, const double *v1, const doub
     MGX_LAUNCH((k_gs_colour<B>), g, dim3(B), s, u, rhs, v1, v2, (int)n, pitch, c, colour);
 }
 
-static void res_grid(long n, dim3 &g, int &R) {
+static void res_grid(long n, long rows, dim3 &g, int &R) {
     const unsigned strips = cdiv(n + 1, 512);
-    const long rows = std::max<long>(n - 1, 1);
+    rows = std::max<long>(rows, 1);
     long want = std::max<long>(1, 4096 / (long)strips);
     R = (int)std::max<long>(8, (rows + want - 1) / want);
     g = dim3(strips, cdiv(rows, R));
 }
 
+static void interior_rows(long n, int ra, int rb, int &f, int &e) {
+    if (rb < 0) {
+        ra = 0;
+        rb = (int)n + 1;
+    }
+    f = std::max(1, ra);
+    e = std::min((int)n, rb);
+}
+
 void launch_residual_norm(const double *u, const double *rhs, const double *v1,
                           const double *v2, long n, long pitch, Coef c, double *partials,
-                          double *out, hipStream_t s) {
+                          double *out, hipStream_t s, int ra, int rb, bool take_sqrt) {
+    int f, e;
+    interior_rows(n, ra, rb, f, e);
     dim3 g;
     int R;
-    res_grid(n, g, R);
+    res_grid(n, e - f, g, R);
     MGX_LAUNCH((k_res_march<0>), g, dim3(256), s, u, rhs, v1, v2, (int)n, pitch, c, R,
-               (double *)nullptr, partials);
+               (double *)nullptr, partials, f, e);
     MGX_LAUNCH(k_norm_final, dim3(1), dim3(kFinalThreads), s, (const double *)partials,
-               (int)(g.x * g.y), out);
+               (int)(g.x * g.y), out, take_sqrt ? 1 : 0);
 }
 
 void launch_residual(double *res, const double *u, const double *rhs, const double *v1,
                      const double *v2, long n, long pitch, Coef c, hipStream_t s) {
+    int f, e;
+    interior_rows(n, 0, -1, f, e);
     dim3 g;
     int R;
-    res_grid(n, g, R);
+    res_grid(n, e - f, g, R);
     MGX_LAUNCH((k_res_march<1>), g, dim3(256), s, u, rhs, v1, v2, (int)n, pitch, c, R, res,
-               (double *)nullptr);
+               (double *)nullptr, f, e);
 }
 
 void launch_rhs(double *rhs, const double *u, const double *v1, const double *v2, long n,
-                long pitch, Coef c, hipStream_t s) {
+                long pitch, Coef c, hipStream_t s, int ra, int rb) {
+    int f, e;
+    interior_rows(n, ra, rb, f, e);
     dim3 g;
     int R;
-    res_grid(n, g, R);
+    res_grid(n, e - f, g, R);
     MGX_LAUNCH((k_res_march<2>), g, dim3(256), s, u, (const double *)nullptr, v1, v2, (int)n,
-               pitch, c, R, rhs, (double *)nullptr);
+               pitch, c, R, rhs, (double *)nullptr, f, e);
 }
 
 void launch_residual_restrict(const double *u, const double *rhs, const double *v1,

@@ -4,21 +4,21 @@
 // for call; every stencil op is a CDNA4 kernel from kernels.hip on the
 // context's stream.  The level towers live in HBM in the "tower layout"
 // (row pitch round_up(n+1,16) doubles); u has two buffers per level because
-// the one-pass smoother is out of place (ping-pong).
+// the one-pass smoother is out of place (ping-pong).  Row-partitioned
+// multi-GPU contexts (ctx->dist) are implemented in dist.hip.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
-#include <algorithm>
 #include <cstring>
 #include <mutex>
 #include <string>
 #include <vector>
 
-#include "../../include/mgx.h"
-#include "kernels.h"
+#include "ctx.h"
 
-namespace {
+namespace mgxi {
 
 thread_local std::string g_err;
 
@@ -26,61 +26,6 @@ int fail(int code, const std::string &msg) {
     g_err = msg;
     return code;
 }
-
-#define HIPCHK(expr)                                                                     \
-    do {                                                                                 \
-        hipError_t e_ = (expr);                                                          \
-        if (e_ != hipSuccess)                                                            \
-            return fail(MGX_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
-    } while (0)
-
-#define CHK(expr)              \
-    do {                       \
-        int rc_ = (expr);      \
-        if (rc_) return rc_;   \
-    } while (0)
-
-struct Level {
-    long n = 0, pitch = 0;
-    double *u[2] = {nullptr, nullptr};
-    int cur = 0;
-    bool zero = false;   // u is logically all zeros (multigrid.cpp:77), not yet written
-    double *rhs = nullptr, *v1 = nullptr, *v2 = nullptr;
-    mgx::Coef coef{};
-    double M() const { return double(n + 1) * double(n + 1); }
-    double *U() const { return u[cur]; }
-};
-
-struct ProfRec {
-    int kind, level;
-    double bytes;
-    hipEvent_t e0, e1;
-};
-
-}  // namespace
-
-struct mgx_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    long N = 0;
-    int L = 0;
-    double dt = 0, nu = 0;
-    mgx_options opt{};
-    std::vector<Level> lv;
-    double *partials = nullptr;   // norm partial sums
-    double *dscal = nullptr;      // [0] norm, [2..3] coarse stats (iterations, last norm)
-    double *hscal = nullptr;      // pinned host mirror
-    double *stage[2] = {nullptr, nullptr};   // reference-layout (N+1)^2 staging
-    // profiling
-    bool prof = false;
-    std::vector<ProfRec> pending;
-    std::vector<hipEvent_t> pool;
-    double sum_ms[MGX_K_COUNT][64] = {};
-    double sum_bytes[MGX_K_COUNT][64] = {};
-    long count[MGX_K_COUNT][64] = {};
-};
-
-namespace {
 
 int check_launch(const char *what) {
     hipError_t e = hipGetLastError();
@@ -97,24 +42,6 @@ hipEvent_t take_event(mgx_ctx *c) {
     hipEvent_t e = nullptr;
     if (hipEventCreate(&e) != hipSuccess) return nullptr;
     return e;
-}
-
-// Launch helper: records HIP events around the launch when profiling is on.
-template <class F>
-int launch(mgx_ctx *c, int kind, int level, double bytes, F &&f) {
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (c->prof) {
-        e0 = take_event(c);
-        e1 = take_event(c);
-        if (e0) (void)hipEventRecord(e0, c->stream);
-    }
-    f();
-    CHK(check_launch("kernel launch"));
-    if (c->prof && e0 && e1) {
-        (void)hipEventRecord(e1, c->stream);
-        c->pending.push_back({kind, level, bytes, e0, e1});
-    }
-    return MGX_OK;
 }
 
 int prof_flush(mgx_ctx *c) {
@@ -244,7 +171,7 @@ int read_norm(mgx_ctx *c, double *norm) {
     return MGX_OK;
 }
 
-int op_residual_norm(mgx_ctx *c, int l, double *norm, double bytes_per_pt = 48.0) {
+int op_residual_norm(mgx_ctx *c, int l, double *norm, double bytes_per_pt) {
     CHK(materialize(c, l));
     Level &L = c->lv[l];
     CHK(launch(c, MGX_K_RESNORM, l, bytes_per_pt * L.M(), [&] {
@@ -308,7 +235,7 @@ int op_coarse(mgx_ctx *c, int l) {
 // mg_inner (multigrid.cpp:17-92).  If norm != nullptr (finest level only) the
 // residual norm after the cycle (multigrid.cpp:112-113) is produced too, fused
 // into the last post-smoothing pass when possible.
-int op_vcycle(mgx_ctx *c, int l, double *norm = nullptr) {
+int op_vcycle(mgx_ctx *c, int l, double *norm) {
     bool have_norm = false;
     for (int sh = 0; sh < c->opt.shape; ++sh) {
         const bool last = sh == c->opt.shape - 1;
@@ -339,12 +266,22 @@ int op_rhs(mgx_ctx *c) {
 }
 
 // mg_outer (multigrid.cpp:97-120).
+// one V-cycle + the residual norm after it, single GPU or partitioned
+int cycle_norm(mgx_ctx *c, double *res) {
+    if (c->dist) return dist_vcycle(c, res);
+    return op_vcycle(c, 0, res);
+}
+int norm0(mgx_ctx *c, double *res) {
+    if (c->dist) return dist_residual_norm(c, res);
+    return op_residual_norm(c, 0, res);
+}
+
 int op_mg_outer(mgx_ctx *c, double tol, int *cycles, double *res0_out, double *res_out) {
     double res0 = 0, res = 0;
-    CHK(op_residual_norm(c, 0, &res0));
+    CHK(norm0(c, &res0));
     res = res0;
     int iter = 0;
-    for (; iter < c->opt.max_cycle && res / res0 > tol; ++iter) CHK(op_vcycle(c, 0, &res));
+    for (; iter < c->opt.max_cycle && res / res0 > tol; ++iter) CHK(cycle_norm(c, &res));
     if (cycles) *cycles = iter;
     if (res0_out) *res0_out = res0;
     if (res_out) *res_out = res;
@@ -396,6 +333,7 @@ int build_tower(mgx_ctx *c) {
 void free_ctx(mgx_ctx *c) {
     if (!c) return;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->dist) dist_free(c);
     for (auto &L : c->lv) {
         (void)hipFree(L.u[0]);
         (void)hipFree(L.u[1]);
@@ -413,7 +351,7 @@ void free_ctx(mgx_ctx *c) {
         (void)hipEventDestroy(r.e1);
     }
     for (auto e : c->pool) (void)hipEventDestroy(e);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
@@ -435,7 +373,9 @@ int raw_scratch(double **p) {
     return MGX_OK;
 }
 
-}  // namespace
+}  // namespace mgxi
+
+using namespace mgxi;
 
 // =================================================================== C ABI
 extern "C" {
@@ -498,8 +438,11 @@ int mgx_compute_rhs(double *rhs, const double *u, long n, const double *v1, cons
     return check_launch("mgx_compute_rhs");
 }
 
+}  // extern "C"
+
 // ---- context
-int mgx_create(mgx_ctx **out, long n, int maxlvl, double dt, double nu, const mgx_options *opt) {
+int mgxi::create_ctx(mgx_ctx **out, long n, int maxlvl, double dt, double nu,
+                     const mgx_options *opt, hipStream_t borrowed) {
     if (!out) return fail(MGX_E_ARG, "mgx_create: null out");
     *out = nullptr;
     if (!is_pow2(n)) return fail(MGX_E_ARG, "mgx_create: n must be a power of two >= 2");
@@ -527,8 +470,12 @@ int mgx_create(mgx_ctx **out, long n, int maxlvl, double dt, double nu, const mg
         if (e != hipSuccess) return bail(fail(MGX_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e)));
     }
     if (hipGetDevice(&c->device) != hipSuccess) return bail(fail(MGX_E_HIP, "hipGetDevice"));
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+    if (borrowed) {
+        c->stream = borrowed;
+        c->own_stream = false;
+    } else if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         return bail(fail(MGX_E_HIP, "hipStreamCreate"));
+    }
     c->lv.resize(maxlvl);
     double h = 1.0 / n;   // dx (multigrid.cpp:194), doubled per level (:49)
     for (int l = 0; l < maxlvl; ++l) {
@@ -562,13 +509,21 @@ int mgx_create(mgx_ctx **out, long n, int maxlvl, double dt, double nu, const mg
     return MGX_OK;
 }
 
+extern "C" {
+
+int mgx_create(mgx_ctx **out, long n, int maxlvl, double dt, double nu, const mgx_options *opt) {
+    return create_ctx(out, n, maxlvl, dt, nu, opt, nullptr);
+}
+
 int mgx_destroy(mgx_ctx *c) {
     free_ctx(c);
     return MGX_OK;
 }
 
-static int upload_impl(mgx_ctx *c, const double *u0, const double *v1, const double *v2,
-                       hipMemcpyKind kind) {
+}  // extern "C"
+
+int mgxi::upload_ctx(mgx_ctx *c, const double *u0, const double *v1, const double *v2,
+                     hipMemcpyKind kind) {
     if (!c || !u0 || !v1 || !v2) return fail(MGX_E_ARG, "mgx_upload: bad args");
     HIPCHK(hipSetDevice(c->device));
     Level &L = c->lv[0];
@@ -589,11 +544,15 @@ static int upload_impl(mgx_ctx *c, const double *u0, const double *v1, const dou
     return MGX_OK;
 }
 
+extern "C" {
+
 int mgx_upload(mgx_ctx *c, const double *u0, const double *v1, const double *v2) {
-    return upload_impl(c, u0, v1, v2, hipMemcpyHostToDevice);
+    if (c && c->dist) return dist_upload(c, u0, v1, v2, hipMemcpyHostToDevice);
+    return upload_ctx(c, u0, v1, v2, hipMemcpyHostToDevice);
 }
 int mgx_upload_device(mgx_ctx *c, const double *u0, const double *v1, const double *v2) {
-    return upload_impl(c, u0, v1, v2, hipMemcpyDeviceToDevice);
+    if (c && c->dist) return dist_upload(c, u0, v1, v2, hipMemcpyDeviceToDevice);
+    return upload_ctx(c, u0, v1, v2, hipMemcpyDeviceToDevice);
 }
 
 static int download_impl(mgx_ctx *c, int level, int field, double *out, hipMemcpyKind kind) {
@@ -610,36 +569,54 @@ static int download_impl(mgx_ctx *c, int level, int field, double *out, hipMemcp
     return MGX_OK;
 }
 
-int mgx_download(mgx_ctx *c, double *u) { return download_impl(c, 0, 0, u, hipMemcpyDeviceToHost); }
+int mgx_download(mgx_ctx *c, double *u) {
+    if (c && c->dist) return dist_download(c, u, hipMemcpyDeviceToHost);
+    return download_impl(c, 0, 0, u, hipMemcpyDeviceToHost);
+}
 int mgx_download_device(mgx_ctx *c, double *u) {
+    if (c && c->dist) return dist_download(c, u, hipMemcpyDeviceToDevice);
     return download_impl(c, 0, 0, u, hipMemcpyDeviceToDevice);
 }
 int mgx_download_level(mgx_ctx *c, int level, int field, double *out) {
+    if (c && c->dist) return fail(MGX_E_ARG, "mgx_download_level: not available on a partitioned context");
     return download_impl(c, level, field, out, hipMemcpyDeviceToHost);
 }
 
+static int no_dist(mgx_ctx *c, const char *what) {
+    return fail(MGX_E_ARG, std::string(what) + ": per-level ops are not available on a "
+                                               "partitioned context (use vcycle/mg_outer/step)");
+}
 int mgx_rhs(mgx_ctx *c) {
     if (!c) return fail(MGX_E_ARG, "null ctx");
+    if (c->dist) return dist_rhs(c);
     return op_rhs(c);
 }
 int mgx_gs(mgx_ctx *c, int level, int sweeps) {
     if (!c || level < 0 || level >= c->L || sweeps < 0) return fail(MGX_E_ARG, "mgx_gs: bad args");
+    if (c->dist) return no_dist(c, "mgx_gs");
     return op_gs(c, level, sweeps);
 }
 int mgx_residual_norm(mgx_ctx *c, int level, double *norm) {
     if (!c || level < 0 || level >= c->L || !norm) return fail(MGX_E_ARG, "mgx_residual_norm: bad args");
+    if (c->dist) {
+        if (level != 0) return no_dist(c, "mgx_residual_norm");
+        return dist_residual_norm(c, norm);
+    }
     return op_residual_norm(c, level, norm);
 }
 int mgx_restrict(mgx_ctx *c, int level) {
     if (!c || level < 0 || level >= c->L - 1) return fail(MGX_E_ARG, "mgx_restrict: bad level");
+    if (c->dist) return no_dist(c, "mgx_restrict");
     return op_restrict(c, level);
 }
 int mgx_prolong_add(mgx_ctx *c, int level) {
     if (!c || level < 0 || level >= c->L - 1) return fail(MGX_E_ARG, "mgx_prolong_add: bad level");
+    if (c->dist) return no_dist(c, "mgx_prolong_add");
     return op_prolong_add(c, level);
 }
 int mgx_vcycle(mgx_ctx *c) {
     if (!c) return fail(MGX_E_ARG, "null ctx");
+    if (c->dist) return dist_vcycle(c, nullptr);
     return op_vcycle(c, 0);
 }
 int mgx_mg_outer(mgx_ctx *c, double tol, int *cycles, double *res0, double *res) {
@@ -648,24 +625,25 @@ int mgx_mg_outer(mgx_ctx *c, double tol, int *cycles, double *res0, double *res)
 }
 int mgx_step(mgx_ctx *c, double tol, int *cycles) {
     if (!c) return fail(MGX_E_ARG, "null ctx");
-    CHK(op_rhs(c));
+    CHK(c->dist ? dist_rhs(c) : op_rhs(c));
     return op_mg_outer(c, tol, cycles, nullptr, nullptr);
 }
 int mgx_run_cycles(mgx_ctx *c, int cycles, double *res) {
     if (!c || cycles < 0) return fail(MGX_E_ARG, "mgx_run_cycles: bad args");
     double r = 0;
-    for (int k = 0; k < cycles; ++k) CHK(op_vcycle(c, 0, &r));
+    for (int k = 0; k < cycles; ++k) CHK(cycle_norm(c, &r));
     if (res) *res = r;
     return MGX_OK;
 }
 
 int mgx_level_n(mgx_ctx *c, int level, long *n) {
     if (!c || !n || level < 0 || level >= c->L) return fail(MGX_E_ARG, "mgx_level_n: bad args");
-    *n = c->lv[level].n;
+    *n = c->N >> level;
     return MGX_OK;
 }
 int mgx_coarse_iterations(mgx_ctx *c, long *iters) {
     if (!c || !iters) return fail(MGX_E_ARG, "bad args");
+    if (c->dist) c = dist_sub(c, 0);   // every rank runs the same replicated coarse solve
     HIPCHK(hipMemcpyAsync(c->hscal + 2, c->dscal + 2, 2 * sizeof(double), hipMemcpyDeviceToHost,
                           c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -687,6 +665,7 @@ int mgx_profile_enable(mgx_ctx *c, int on) {
     if (!c) return fail(MGX_E_ARG, "null ctx");
     CHK(prof_flush(c));
     c->prof = on != 0;
+    for (int i = 0; i < dist_nsub(c); ++i) CHK(mgx_profile_enable(dist_sub(c, i), on));
     return MGX_OK;
 }
 int mgx_profile_reset(mgx_ctx *c) {
@@ -695,8 +674,11 @@ int mgx_profile_reset(mgx_ctx *c) {
     memset(c->sum_ms, 0, sizeof(c->sum_ms));
     memset(c->sum_bytes, 0, sizeof(c->sum_bytes));
     memset(c->count, 0, sizeof(c->count));
+    for (int i = 0; i < dist_nsub(c); ++i) CHK(mgx_profile_reset(dist_sub(c, i)));
     return MGX_OK;
 }
+// Partitioned contexts: the replicated levels' launches (sub-contexts, level
+// numbers shifted by the first replicated level) are included.
 int mgx_profile_get(mgx_ctx *c, int kind, int level, long *launches, double *ms, double *bytes) {
     if (!c || kind < 0 || kind >= MGX_K_COUNT || level >= 64)
         return fail(MGX_E_ARG, "mgx_profile_get: bad args");
@@ -708,6 +690,16 @@ int mgx_profile_get(mgx_ctx *c, int kind, int level, long *launches, double *ms,
         n += c->count[kind][l];
         t += c->sum_ms[kind][l];
         b += c->sum_bytes[kind][l];
+    }
+    const int la = dist_la(c);
+    for (int i = 0; i < dist_nsub(c); ++i) {
+        if (level >= 0 && level < la) break;
+        long sn = 0;
+        double st = 0, sb = 0;
+        CHK(mgx_profile_get(dist_sub(c, i), kind, level < 0 ? -1 : level - la, &sn, &st, &sb));
+        n += sn;
+        t += st;
+        b += sb;
     }
     if (launches) *launches = n;
     if (ms) *ms = t;
@@ -803,6 +795,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgx::set_march_block(value);
         return MGX_OK;
     }
+    if (!strcmp(key, "dist_min_rows")) {
+        if (value < 16 || (value & 1)) return fail(MGX_E_ARG, "dist_min_rows must be even, >= 16");
+        mgxi::g_dist_min_rows = value;
+        return MGX_OK;
+    }
     return fail(MGX_E_ARG, std::string("mgx_set_tuning: unknown key ") + key);
 }
 extern "C" int mgx_get_tuning(const char *key, long *value) {
@@ -813,6 +810,10 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "march_block")) {
         *value = mgx::get_march_block();
+        return MGX_OK;
+    }
+    if (!strcmp(key, "dist_min_rows")) {
+        *value = mgxi::g_dist_min_rows;
         return MGX_OK;
     }
     return fail(MGX_E_ARG, std::string("mgx_get_tuning: unknown key ") + key);

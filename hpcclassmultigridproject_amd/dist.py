@@ -1,0 +1,51 @@
+"""Multi-GPU plumbing for the row-partitioned solver.
+
+One process per GPU.  libmgx owns the RCCL communicator; torch.distributed
+only brokers the 128-byte unique id from rank 0 (any backend, gloo included)
+and reads RANK / WORLD_SIZE / LOCAL_RANK.  The partition plan is computed by
+libmgx (``mgx_partition``) so that host code and kernels agree on it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from . import _lib
+from ._lib import check, lib
+
+
+def env_rank():
+    """-> (rank, world, local_rank) from the torch.distributed.run environment."""
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)),
+            int(os.environ.get("LOCAL_RANK", 0)))
+
+
+def unique_id() -> bytes:
+    """A fresh RCCL unique id (call on ONE rank, share with the others)."""
+    buf = C.create_string_buffer(_lib.UNIQUE_ID_BYTES)
+    check(lib().mgx_dist_unique_id(buf))
+    return buf.raw
+
+
+def broadcast_unique_id(group=None) -> bytes:
+    """Make the id on rank 0 and broadcast it over torch.distributed."""
+    import torch
+    import torch.distributed as dist
+
+    rank = dist.get_rank(group)
+    payload = torch.zeros(_lib.UNIQUE_ID_BYTES, dtype=torch.uint8)
+    if rank == 0:
+        payload[:] = torch.frombuffer(bytearray(unique_id()), dtype=torch.uint8)
+    backend = dist.get_backend(group)
+    if backend == "nccl":   # RCCL broadcasts device tensors only
+        payload = payload.cuda()
+    dist.broadcast(payload, src=0, group=group)
+    return bytes(payload.cpu().numpy().tobytes())
+
+
+def partition(n: int, maxlvl: int, world: int, rank: int, level: int):
+    """-> (ra, rb, first_replicated_level): rows [ra, rb) of `level` on `rank`."""
+    ra, rb, la = C.c_int(), C.c_int(), C.c_int()
+    check(lib().mgx_partition(n, maxlvl, world, rank, level, C.byref(ra), C.byref(rb),
+                              C.byref(la)))
+    return ra.value, rb.value, la.value

@@ -51,19 +51,43 @@ def timestepper(uT, u0, v1, v2, nu, maxlvl, n, dt, T, dx, tol, shape=1, *, nsmoo
 
 
 class Multigrid:
-    """Device-resident level towers and the V-cycle (mgx_ctx)."""
+    """Device-resident level towers and the V-cycle (mgx_ctx).
+
+    Row-partitioned multi-GPU: ``world > 1`` with ``rank`` and the
+    ``unique_id`` from ``dist.unique_id()`` (one process per GPU, RCCL), or
+    ``local_parts=G`` for G virtual ranks on this GPU.  A partitioned solver
+    takes the whole-solver calls (upload/download of the full grid, rhs,
+    mg_inner, mg_outer, step, run_cycles, residual_norm(0)).
+    """
 
     def __init__(self, N, maxlvl, dt, nu, *, nsmooth=3, shape=1,
                  tower_mode=_lib.TOWER_REFERENCE, device=-1, smoother=0, fuse=3,
-                 coarse_tol=1e-5, coarse_maxit=1000, max_cycle=50):
+                 coarse_tol=1e-5, coarse_maxit=1000, max_cycle=50,
+                 world=1, rank=0, unique_id=None, local_parts=0):
         self.N, self.maxlvl, self.dt, self.nu = N, maxlvl, dt, nu
         self.opt = default_options(nsmooth=nsmooth, shape=shape, tower_mode=tower_mode,
                                    device=device, smoother=smoother, fuse=fuse,
                                    coarse_tol=coarse_tol,
                                    coarse_maxit=coarse_maxit, max_cycle=max_cycle)
         h = C.c_void_p()
-        check(lib().mgx_create(C.byref(h), N, maxlvl, dt, nu, C.byref(self.opt)))
+        if local_parts:
+            check(lib().mgx_create_local_dist(C.byref(h), N, maxlvl, dt, nu,
+                                              C.byref(self.opt), local_parts))
+        elif world > 1 or unique_id is not None:
+            if unique_id is None or len(unique_id) != _lib.UNIQUE_ID_BYTES:
+                raise ValueError("world > 1 needs the 128-byte unique_id from rank 0")
+            idbuf = C.create_string_buffer(bytes(unique_id), _lib.UNIQUE_ID_BYTES)
+            check(lib().mgx_create_dist(C.byref(h), N, maxlvl, dt, nu, C.byref(self.opt),
+                                        rank, world, idbuf))
+        else:
+            check(lib().mgx_create(C.byref(h), N, maxlvl, dt, nu, C.byref(self.opt)))
         self._h = h
+
+    def dist_info(self):
+        """-> (world, rank, first replicated level); rank -1 for local parts."""
+        w, r, la = C.c_int(), C.c_int(), C.c_int()
+        check(lib().mgx_dist_info(self._h, C.byref(w), C.byref(r), C.byref(la)))
+        return w.value, r.value, la.value
 
     # -- lifetime
     def close(self):

@@ -156,7 +156,9 @@ int mgx_synchronize(mgx_ctx *ctx);
 /* Process-wide tuning knobs.  "tile_max_n": levels with n <= value run the
  * fused smoothing pass as 2-D LDS tiles instead of the row march (default 2048;
  * env MGX_TILE_MAX_N).  "march_block": lanes per workgroup of the row march on
- * levels with n >= 4096, 128 or 256 (default 256; env MGX_MARCH_BLOCK). */
+ * levels with n >= 4096, 128 or 256 (default 256; env MGX_MARCH_BLOCK).
+ * "dist_min_rows": partitioned solvers replicate every level whose row blocks
+ * would be shorter than this (default 256, even, >= 16); read at creation. */
 int mgx_set_tuning(const char *key, long value);
 int mgx_get_tuning(const char *key, long *value);
 
@@ -176,6 +178,35 @@ int mgx_profile_reset(mgx_ctx *ctx);
  * device milliseconds, summed algorithmic bytes (SURVEY 8d byte model). */
 int mgx_profile_get(mgx_ctx *ctx, int kind, int level, long *launches, double *ms,
                     double *bytes);
+
+/* ---- Row-partitioned multi-GPU solver ---------------------------
+ * The finest levels are split into contiguous row blocks, one per rank, with
+ * ghost rows refreshed once per fused smoothing pass; levels whose blocks
+ * would be shorter than 256 rows are replicated on every rank (the restricted
+ * rhs is all-gathered).  u after any number of V-cycles is bitwise the
+ * single-GPU (and reference) result; the residual norm is an all-reduced sum.
+ * A partitioned context takes every whole-solver call (upload/download of the
+ * full grid, rhs, vcycle, mg_outer, step, run_cycles, residual_norm at level
+ * 0); the per-level calls (gs, restrict, prolong_add, download_level) return
+ * MGX_E_ARG.  Needs smoother 0, nsmooth >= 1, world a power of two. */
+#define MGX_UNIQUE_ID_BYTES 128
+/* RCCL unique id (128 bytes) made on one rank and shared with the others. */
+int mgx_dist_unique_id(void *id128);
+/* One rank of `world` (one process per GPU; select the GPU with opt->device).
+ * Collective: every rank must call it with the same id, n, maxlvl, options. */
+int mgx_create_dist(mgx_ctx **out, long n, int maxlvl, double dt, double nu,
+                    const mgx_options *opt, int rank, int world, const void *id128);
+/* `world` virtual ranks in this process on one GPU, ghost exchanges as
+ * device copies (tests the partition on a single GPU). */
+int mgx_create_local_dist(mgx_ctx **out, long n, int maxlvl, double dt, double nu,
+                          const mgx_options *opt, int world);
+/* Partition plan (host only): owned rows [*ra, *rb) of `level` on `rank`, and
+ * the first replicated level (levels >= it are whole on every rank). */
+int mgx_partition(long n, int maxlvl, int world, int rank, int level, int *ra, int *rb,
+                  int *replicated_level);
+/* world size, rank (-1 for a local multi-part context; 0/1 for single GPU),
+ * first replicated level (maxlvl for a single-GPU context). */
+int mgx_dist_info(mgx_ctx *ctx, int *world, int *rank, int *replicated_level);
 
 #ifdef __cplusplus
 }
