@@ -27,20 +27,28 @@ def unique_id() -> bytes:
     return buf.raw
 
 
-def broadcast_unique_id(group=None) -> bytes:
-    """Make the id on rank 0 and broadcast it over torch.distributed."""
+def broadcast_bytes(data, nbytes: int, group=None) -> bytes:
+    """Broadcast `nbytes` bytes from rank 0 (data is ignored on other ranks)."""
     import torch
     import torch.distributed as dist
 
-    rank = dist.get_rank(group)
-    payload = torch.zeros(_lib.UNIQUE_ID_BYTES, dtype=torch.uint8)
-    if rank == 0:
-        payload[:] = torch.frombuffer(bytearray(unique_id()), dtype=torch.uint8)
-    backend = dist.get_backend(group)
-    if backend == "nccl":   # RCCL broadcasts device tensors only
+    payload = torch.zeros(nbytes, dtype=torch.uint8)
+    if dist.get_rank(group) == 0:
+        if data is None or len(data) != nbytes:
+            raise ValueError(f"rank 0 must supply {nbytes} bytes")
+        payload[:] = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+    if dist.get_backend(group) == "nccl":   # RCCL broadcasts device tensors only
         payload = payload.cuda()
     dist.broadcast(payload, src=0, group=group)
     return bytes(payload.cpu().numpy().tobytes())
+
+
+def broadcast_unique_id(group=None) -> bytes:
+    """Make the RCCL id on rank 0 and broadcast it over torch.distributed."""
+    import torch.distributed as dist
+
+    uid = unique_id() if dist.get_rank(group) == 0 else None
+    return broadcast_bytes(uid, _lib.UNIQUE_ID_BYTES, group)
 
 
 def partition(n: int, maxlvl: int, world: int, rank: int, level: int):

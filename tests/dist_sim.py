@@ -1,0 +1,173 @@
+"""CPU model of the row-partitioned V-cycle (dist.hip), for gloo tests.
+
+Test infrastructure: every rank holds each partitioned level as a full-size
+array of which only its allocated rows [lo, hi] (owned rows + kGhost ghost
+rows, as in dist.hip) are meaningful; every other row is POISONED with NaN
+before each smoothing pass, so any dependence on data the rank does not hold
+shows up as NaN in its owned rows.  The stencil arithmetic is the oracle's
+(oracle/mg_oracle.c, the reference's term order), the data movement is what
+dist.hip does, over torch.distributed (gloo): ghost rows from rank +-1
+(isend/irecv), all-gather of the restricted rhs into the first replicated
+level, all-reduce of the residual's sum of squares.  The partition plan comes
+from libmgx's own mgx_partition.
+
+Mirrors: dist.hip dist_level (pre pass + restrict, recurse / gather, post
+pass + prolong), multigrid.cpp:17-92 for the replicated levels.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from oracle import oracle as O
+
+K_GHOST = 8   # dist.hip kGhost
+
+
+class Block:
+    def __init__(self, n, ra, rb):
+        self.n, self.ra, self.rb = n, ra, rb
+        self.lo = max(0, ra - K_GHOST)
+        self.hi = min(n, rb - 1 + K_GHOST)
+
+    def rows(self, a):
+        return a.reshape(self.n + 1, self.n + 1)
+
+    def poison(self, a):
+        m = self.rows(a)
+        m[: self.lo] = np.nan
+        m[self.hi + 1:] = np.nan
+
+
+def exchange(blk, a, rank, world):
+    """Ghost rows [lo, ra) from rank-1 and [rb, hi] from rank+1 (dist.hip exchange)."""
+    m = blk.rows(a)
+    reqs, recv = [], []
+    if rank > 0:
+        g = blk.ra - blk.lo
+        reqs.append(dist.isend(torch.from_numpy(m[blk.ra:blk.ra + g].copy()), rank - 1))
+        buf = torch.empty((g, blk.n + 1), dtype=torch.float64)
+        reqs.append(dist.irecv(buf, rank - 1))
+        recv.append((blk.lo, buf))
+    if rank < world - 1:
+        g = blk.hi - blk.rb + 1
+        reqs.append(dist.isend(torch.from_numpy(m[blk.rb - g:blk.rb].copy()), rank + 1))
+        buf = torch.empty((g, blk.n + 1), dtype=torch.float64)
+        reqs.append(dist.irecv(buf, rank + 1))
+        recv.append((blk.rb, buf))
+    for r in reqs:
+        r.wait()
+    for r0, buf in recv:
+        m[r0:r0 + buf.shape[0]] = buf.numpy()
+
+
+class PartitionedVCycle:
+    def __init__(self, rank, world, N, L, tower, dt, nu, nsmooth, plan):
+        """plan(level) -> (ra, rb, la): mgx_partition for this rank."""
+        self.rank, self.world, self.N, self.L = rank, world, N, L
+        self.dt, self.nu, self.nsmooth = dt, nu, nsmooth
+        self.la = plan(0)[2]
+        self.blk = [Block(N >> l, *plan(l)[:2]) for l in range(self.la)]
+        self.v1 = [tower.level("v1", l) for l in range(L)]
+        self.v2 = [tower.level("v2", l) for l in range(L)]
+        self.u = [np.zeros((N >> l) ** 2 + 2 * (N >> l) + 1) for l in range(L)]
+        self.rhs = [np.zeros_like(x) for x in self.u]
+        self.coarse_iters = 0
+
+    def h(self, l):
+        return (1.0 / self.N) * 2 ** l
+
+    def _gs(self, l):
+        n = self.N >> l
+        for _ in range(self.nsmooth):
+            O.gauss_seidel(self.u[l], self.rhs[l], n, self.v1[l], self.v2[l], self.dt, self.nu,
+                           self.h(l))
+
+    def _res(self, l):
+        n = self.N >> l
+        return O.residual(self.u[l], self.rhs[l], n, self.v1[l], self.v2[l], self.dt, self.nu,
+                          self.h(l))
+
+    # -- replicated levels (multigrid.cpp:17-92 on whole arrays)
+    def _full(self, l):
+        n = self.N >> l
+        if l == self.L - 1:
+            res, i = 1.0, 0
+            while i < 1000 and res > 1e-5:
+                O.gauss_seidel(self.u[l], self.rhs[l], n, self.v1[l], self.v2[l], self.dt,
+                               self.nu, self.h(l))
+                res = O.compute_norm(self._res(l), n)
+                i += 1
+            self.coarse_iters += i
+            return
+        self._gs(l)
+        self.rhs[l + 1] = O.restriction(self._res(l), n)
+        self.u[l + 1][:] = 0.0
+        self._full(l + 1)
+        self.u[l] += O.prolongation(self.u[l + 1], n // 2)
+        self._gs(l)
+
+    # -- partitioned levels (dist.hip dist_level)
+    def _level(self, l, zero, want_norm):
+        n, b = self.N >> l, self.blk[l]
+        # pre-smoothing pass (+ residual restricted to the coarse rhs)
+        if zero:
+            self.u[l][:] = 0.0
+        else:
+            exchange(b, self.u[l], self.rank, self.world)
+        b.poison(self.u[l])
+        b.poison(self.rhs[l])
+        self._gs(l)
+        res = self._res(l)
+        crs = O.restriction(res, n)   # coarse rows I <- fine rows 2I
+        nc = n // 2
+        c = crs.reshape(nc + 1, nc + 1)
+        tgt = self.rhs[l + 1].reshape(nc + 1, nc + 1)
+        own = slice((b.ra + 1) // 2, (b.rb + 1) // 2)   # I with 2I in [ra, rb)
+        tgt[own] = c[own]
+        if l + 1 < self.la:
+            exchange(self.blk[l + 1], self.rhs[l + 1], self.rank, self.world)
+            self._level(l + 1, True, False)
+        else:
+            self._gather_rhs(l + 1)
+            self.u[l + 1][:] = 0.0
+            self._full(l + 1)
+        # post-smoothing pass: prolongation + add, sweeps (+ residual norm)
+        exchange(b, self.u[l], self.rank, self.world)
+        if l + 1 < self.la:
+            exchange(self.blk[l + 1], self.u[l + 1], self.rank, self.world)
+            self.blk[l + 1].poison(self.u[l + 1])
+        b.poison(self.u[l])
+        self.u[l] += O.prolongation(self.u[l + 1], nc)
+        self._gs(l)
+        if want_norm:
+            r = self._res(l).reshape(n + 1, n + 1)
+            i0, i1 = max(1, b.ra), min(n, b.rb)
+            part = torch.tensor([float(np.sum(r[i0:i1, 1:n] ** 2))], dtype=torch.float64)
+            dist.all_reduce(part)
+            return math.sqrt(float(part[0]))
+        return None
+
+    def _gather_rhs(self, l):
+        n = self.N >> l
+        q = n // self.world
+        m = self.rhs[l].reshape(n + 1, n + 1)
+        mine = torch.from_numpy(m[self.rank * q:(self.rank + 1) * q].copy())
+        parts = [torch.empty_like(mine) for _ in range(self.world)]
+        dist.all_gather(parts, mine)
+        for r, t in enumerate(parts):
+            m[r * q:(r + 1) * q] = t.numpy()
+
+    def vcycle(self):
+        """One V-cycle from u[0], rhs[0]; returns the all-reduced residual norm."""
+        if self.la == 0:
+            self._full(0)
+            return O.compute_norm(self._res(0), self.N)
+        return self._level(0, False, True)
+
+    def owned(self, a, l=0):
+        b = self.blk[l] if l < self.la else Block(self.N >> l, 0, (self.N >> l) + 1)
+        return b.rows(a)[b.ra:b.rb]

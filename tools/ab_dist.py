@@ -1,0 +1,41 @@
+"""Cost of the row partition on one GPU: ms per V-cycle (+norm) for the single
+context vs G virtual ranks (mgx_create_local_dist), per-kind device times.
+The virtual ranks run one after another on one stream, so G parts ~ 1 GPU's
+work + the partition overheads (ghost rows recomputed, exchanges, more
+launches, replicated coarse levels G times).
+    python tools/ab_dist.py [--N 16384 --L 9] [--parts 1,2,4,8] [--cycles 5]"""
+import argparse, json, sys, time
+sys.path.insert(0, '.')
+import hpcclassmultigridproject_amd as pkg
+from hpcclassmultigridproject_amd import _lib
+ap = argparse.ArgumentParser()
+ap.add_argument('--N', type=int, default=16384)
+ap.add_argument('--L', type=int, default=9)
+ap.add_argument('--parts', default='1,2,4,8')
+ap.add_argument('--cycles', type=int, default=5)
+ap.add_argument('--rounds', type=int, default=2)
+a = ap.parse_args()
+N, L = a.N, a.L
+dt = 1.0 / N / 10
+u0, v1, v2 = pkg.init_problem(N, nthreads=16)
+for rnd in range(a.rounds):
+    for G in [int(x) for x in a.parts.split(',')]:
+        mg = pkg.Multigrid(N, L, dt, -4e-4, device=0, local_parts=G if G > 1 else 0)
+        mg.upload(u0, v1, v2); mg.rhs(); mg.run_cycles(1); mg.synchronize()
+        mg.profile_reset(); mg.profile(True)
+        t = time.perf_counter(); r = mg.run_cycles(a.cycles); mg.synchronize()
+        ms = (time.perf_counter() - t) / a.cycles * 1e3
+        d = {"G": G, "ms": round(ms, 3), "la": mg.dist_info()[2], "res": r}
+        for kind, name in _lib.KERNEL_NAMES.items():
+            n, kms, _ = mg.profile_get(kind, -1)
+            if n: d[name] = round(kms / a.cycles, 4)
+        lv = []
+        for l in range(L):
+            t = 0.0
+            for kind in _lib.KERNEL_NAMES:
+                n, kms, _ = mg.profile_get(kind, l)
+                t += kms
+            lv.append(round(t / a.cycles, 4))
+        d["per_level_ms"] = lv
+        mg.profile(False); mg.close()
+        print(rnd, json.dumps(d), flush=True)
