@@ -1,0 +1,48 @@
+"""The C++ drivers over the C ABI on the GPU (SURVEY 8b caller contracts, 8f).
+
+./multigrid (driver/multigrid.cpp) with the reference's defaults at N=32 must
+write uT.txt and uTomp.txt byte-identical to the reference's own result in
+the reference's format (tests/golden/uT_N32.txt), print the reference's
+lines, and report zero difference between its op-level control flow and the
+library's fast path.  ./mg_sweep writes cudatime.txt / gpups.txt in the
+"N<TAB>value" format speedupplot.py reads.
+"""
+import os
+import subprocess
+
+import pytest
+from conftest import GOLDEN, ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _built(name):
+    exe = os.path.join(ROOT, name)
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "driver")], check=True)
+    return exe
+
+
+def test_multigrid_driver_writes_reference_uT(tmp_path):
+    exe = _built("multigrid")
+    out = subprocess.run([exe, "-N", "32", "-out", str(tmp_path) + "/"], capture_output=True,
+                         text=True, timeout=300, check=True).stdout
+    with open(os.path.join(GOLDEN, "uT_N32.txt")) as f:
+        want = f.read()
+    for name in ("uT.txt", "uTomp.txt"):
+        with open(tmp_path / name) as f:
+            assert f.read() == want, name
+    assert "time, N = 32:" in out
+    assert "Error (compared to the referenced solution) = 0.000000e+00" in out
+
+
+def test_mg_sweep_formats(tmp_path):
+    exe = _built("mg_sweep")
+    out = subprocess.run([exe, "-Nmin", "32", "-Nmax", "256", "-cycles", "2", "-steps", "5",
+                          "-out", str(tmp_path) + "/"], capture_output=True, text=True,
+                         timeout=300, check=True).stdout
+    assert out.count("Time elapsed for grid size") == 4
+    for name, conv in (("cudatime.txt", float), ("gpups.txt", float)):
+        rows = [l.split("\t") for l in open(tmp_path / name).read().splitlines()]
+        assert [int(r[0]) for r in rows] == [32, 64, 128, 256]
+        assert all(conv(r[1]) > 0 for r in rows)
