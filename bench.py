@@ -144,7 +144,9 @@ def main():
     mg.synchronize()
     mg.profile_reset()
     if not args.no_profile:
-        mg.profile(True)
+        # HIP events around the finest-level launches only (the dominant
+        # kernels); events around every small-level launch would cost ~7%
+        mg.profile(True, finest_only=True)
 
     barrier()
     torch.cuda.synchronize()
@@ -161,25 +163,34 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # per-kernel HIP-event timings from the timed region
-    kernels = {}
-    for kind, name in _lib.KERNEL_NAMES.items():
-        n, ms, b = mg.profile_get(kind, -1)
-        if n:
-            kernels[name] = {"launches": n, "ms_per_step": round(ms / args.steps, 4),
-                             "algo_GBs": round(b / (ms * 1e-3) / 1e9, 1) if ms > 0 else None}
-            for lvl in range(L):
-                nl, msl, bl = mg.profile_get(kind, lvl)
-                if nl:
-                    kernels[name][f"L{lvl}_ms_per_step"] = round(msl / args.steps, 4)
-    # dominant kernel = the (kind, level) with the largest device time
+    # dominant kernel = the finest-level (kind) with the largest device time
+    # in the timed region
     best = None
     for kind in _lib.KERNEL_NAMES:
-        for lvl in range(L):
-            n, ms, b = mg.profile_get(kind, lvl)
-            if n and (best is None or ms > best[3]):
-                best = (kind, lvl, n, ms, b)
+        n, ms, b = mg.profile_get(kind, 0)
+        if n and (best is None or ms > best[3]):
+            best = (kind, 0, n, ms, b)
     mg.profile(False)
+
+    # per-kernel, per-level breakdown: a few more cycles, every launch timed
+    # (after the timed region, so its event overhead is not in `value`)
+    kernels = {}
+    if not args.no_profile:
+        prof_steps = 3
+        mg.profile_reset()
+        mg.profile(True)
+        mg.run_cycles(prof_steps)
+        for kind, name in _lib.KERNEL_NAMES.items():
+            n, ms, b = mg.profile_get(kind, -1)
+            if n:
+                kernels[name] = {"launches_per_step": n / prof_steps,
+                                 "ms_per_step": round(ms / prof_steps, 4),
+                                 "algo_GBs": round(b / (ms * 1e-3) / 1e9, 1) if ms > 0 else None}
+                for lvl in range(L):
+                    nl, msl, bl = mg.profile_get(kind, lvl)
+                    if nl:
+                        kernels[name][f"L{lvl}_ms_per_step"] = round(msl / prof_steps, 4)
+        mg.profile(False)
     mg.close()
 
     roof = None
@@ -210,11 +221,22 @@ def main():
             roof["hbm_frac"] = round(traffic / avg_s / 1e9 / HBM_PEAK_GBS, 4)
 
     value = (N - 1) ** 2 * args.steps / elapsed
+    # SURVEY 8d secondary metric: RB-GS point updates per second
+    smoother_pts = sum(2 * args.nsmooth * ((N >> l) - 1) ** 2 for l in range(L - 1))
+    if roof is not None and rank == 0:
+        # measured ceilings (mgx_stream_bandwidth): a copy, and the smoother's
+        # 4-in/1-out stream shape; hbm_frac_of_stream = measured traffic rate
+        # over the latter
+        roof["copy_ceiling_GBs"] = round(_lib.stream_bandwidth(1 << 30, 1, 10), 1)
+        roof["stream5_ceiling_GBs"] = round(_lib.stream_bandwidth(1 << 30, 4, 10), 1)
+        if "hbm_GBs" in roof:
+            roof["hbm_frac_of_stream5"] = round(roof["hbm_GBs"] / roof["stream5_ceiling_GBs"], 4)
     out = {
         "metric": "V-cycle grid-point-updates/sec at N=16384; achieved HBM GB/s vs peak",
         "value": value, "unit": "grid-point-updates/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "smoother_point_updates_per_s": smoother_pts * args.steps / elapsed,
         "scaling": "weak" if (args.weak or world == 1) else "strong",
         "vs_baseline": None, "dtype": "f64",
         "data": "synthetic: the reference problem (Gaussian u0, rotating velocity), "

@@ -78,6 +78,7 @@ _SIGS = {
     "mgx_profile_reset": (_I, [_vp]),
     "mgx_profile_get": (_I, [_vp, _I, _I, C.POINTER(_L), _dp, _dp]),
     "mgx_set_tuning": (_I, [C.c_char_p, _L]),
+    "mgx_stream_bandwidth": (_I, [_L, _I, _I, _dp]),
     "mgx_dist_unique_id": (_I, [_vp]),
     "mgx_create_dist": (_I, [C.POINTER(_vp), _L, _I, _D, _D, C.POINTER(Options), _I, _I, _vp]),
     "mgx_create_local_dist": (_I, [C.POINTER(_vp), _L, _I, _D, _D, C.POINTER(Options), _I]),
@@ -129,3 +130,10 @@ def get_tuning(key: str) -> int:
     v = C.c_long()
     check(lib().mgx_get_tuning(key.encode(), C.byref(v)))
     return v.value
+
+
+def stream_bandwidth(bytes_per_stream=1 << 30, nin=1, reps=10) -> float:
+    """Measured streaming GB/s (mgx_stream_bandwidth): nin=1 copy, nin=4 smoother shape."""
+    g = C.c_double()
+    check(lib().mgx_stream_bandwidth(bytes_per_stream, nin, reps, C.byref(g)))
+    return g.value

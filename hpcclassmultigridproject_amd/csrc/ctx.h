@@ -63,7 +63,7 @@ struct mgx_ctx {
     double *stage[2] = {nullptr, nullptr};   // reference-layout (N+1)^2 staging
     mgxi::Dist *dist = nullptr;   // row-partitioned multi-GPU state (dist.hip)
     // profiling
-    bool prof = false;
+    int prof = 0;   // 0 off, 1 every launch, 2 finest-level launches only
     std::vector<mgxi::ProfRec> pending;
     std::vector<hipEvent_t> pool;
     double sum_ms[MGX_K_COUNT][64] = {};
@@ -79,14 +79,15 @@ hipEvent_t take_event(mgx_ctx *c);
 template <class F>
 int launch(mgx_ctx *c, int kind, int level, double bytes, F &&f) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (c->prof) {
+    const bool rec = c->prof == 1 || (c->prof == 2 && level == 0);
+    if (rec) {
         e0 = take_event(c);
         e1 = take_event(c);
         if (e0) (void)hipEventRecord(e0, c->stream);
     }
     f();
     CHK(check_launch("kernel launch"));
-    if (c->prof && e0 && e1) {
+    if (rec && e0 && e1) {
         (void)hipEventRecord(e1, c->stream);
         c->pending.push_back({kind, level, bytes, e0, e1});
     }

@@ -37,6 +37,9 @@ void launch_injection(double *dst, long dst_pitch, const double *src, long src_p
 // deterministic two-stage reduction; result written to *out (device) as sqrt.
 // `partials` must hold norm_partials_size() doubles.
 int norm_partials_size();
+// bandwidth probe: nin (1 or 4) double2 input streams -> one output stream
+void launch_stream(const double *a, const double *b, const double *c, const double *d,
+                   double *o, long n2, int nin, int grid, hipStream_t s);
 void launch_norm(const double *res, long n, long pitch, double *partials, double *out,
                  hipStream_t s);
 
@@ -81,6 +84,8 @@ void set_tile_max_n(long v);
 long get_tile_max_n();
 // Workgroup width (lanes) of the row march on levels with n >= 4096: 128 or 256.
 void set_march_block(long v);
+void set_march_kernel(long v);
+long get_march_kernel();
 long get_march_block();
 // One colour, in place (two launches make a sweep).  Reference for A/B timing.
 void launch_gs_colour(double *u, const double *rhs, const double *v1, const double *v2,

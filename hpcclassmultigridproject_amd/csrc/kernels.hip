@@ -64,6 +64,29 @@ __device__ __forceinline__ double2 ld2(const double *p) {
 __device__ __forceinline__ void st2(double *p, double2 v) {
     *reinterpret_cast<double2 *>(p) = v;
 }
+// Streaming (non-temporal) forms for data touched once per pass: the fused
+// smoother's rhs/v1/v2/u rows and its output rows.  MGX_NT=0 turns them into
+// plain accesses (A/B builds).
+#ifndef MGX_NT
+#define MGX_NT 1
+#endif
+typedef double mgx_d2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double2 ld2s(const double *p) {
+#if MGX_NT
+    const mgx_d2v v = __builtin_nontemporal_load(reinterpret_cast<const mgx_d2v *>(p));
+    return make_double2(v.x, v.y);
+#else
+    return ld2(p);
+#endif
+}
+__device__ __forceinline__ void st2s(double *p, double2 v) {
+#if MGX_NT
+    const mgx_d2v w = {v.x, v.y};
+    __builtin_nontemporal_store(w, reinterpret_cast<mgx_d2v *>(p));
+#else
+    st2(p, v);
+#endif
+}
 __device__ __forceinline__ double sel(double2 p, int s) {
     const double x = p.x, y = p.y;
     return s ? y : x;
@@ -443,9 +466,13 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
     int strips, long units_per_wg, Coef c, int ra, int rb, int lo, int hi) {
     using C = SmoothCfg<K, MODE>;
     constexpr int S = C::S, E = C::E, H = C::H, NR = C::NR, NS = C::NS;
-    constexpr int LW = 2 * BLOCK + 2;   // LDS row: x = 1 + 2*lane + cs
+    // LDS row = two planes, even and odd columns: lane l's pair (2c, 2c+1)
+    // sits at index l+1 of each, so every stage and residual access is a
+    // unit-stride 8-B word per lane (bank-conflict free; the interleaved
+    // layout's 16-B lane stride cost ~28% of LDS cycles in conflicts)
+    constexpr int LP = BLOCK + 2;
     constexpr int W = 2 * (BLOCK - 2 * H);
-    __shared__ __attribute__((aligned(16))) double ring[NR][LW];
+    __shared__ __attribute__((aligned(16))) double ring[NR][2][LP];
 
     const int l = threadIdx.x;
     const int nrows = rb - ra;
@@ -468,7 +495,7 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
         // per-lane interior flags of the two columns of the pair
         const bool in0 = act && c0 >= 1 && c0 <= n - 1;
         const bool in1 = act && c0 + 1 <= n - 1;
-        const int x0 = 1 + 2 * l;
+        const int pl = l + 1;   // plane index of this lane's pair
 
         // Prefetched u rows (+ coarse operands of their prolongation): row R
         // lives in set R & 1 from its load at step R-5 to its LDS store at step
@@ -489,7 +516,7 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
         auto load_u = [&](int R, UPre &u) {
             if (C::ZERO) return;
             const int Rc = min(max(R, lo), hi);
-            u.X = ld2((uin + (long)Rc * pitch) + cl);
+            u.X = ld2s((uin + (long)Rc * pitch) + cl);
             if (C::PROL) {
                 // branch-free: even rows read coarse row R/2 twice (cache hits)
                 const double *p0 = (uc + (long)(Rc >> 1) * pitchc) + jl;
@@ -517,13 +544,14 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
                 v.x = v.x + pr.x;
                 v.y = v.y + pr.y;
             }
-            st2(&ring[sl][x0], v);
+            ring[sl][0][pl] = v.x;
+            ring[sl][1][pl] = v.y;
         };
         auto load_rv = [&](int R, RowData &d) {
             const long o = (long)min(max(R, lo), hi) * pitch;   // scalar row offset
-            d.r = ld2((rhs + o) + cl);
-            d.x = ld2((v1 + o) + cl);
-            d.y = ld2((v2 + o) + cl);
+            d.r = ld2s((rhs + o) + cl);
+            d.x = ld2s((v1 + o) + cl);
+            d.y = ld2s((v2 + o) + cl);
         };
 
         const int s_first = a - E;
@@ -576,12 +604,15 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
                     const bool inr = r >= 1 && r <= n - 1;
                     if (inr && (cs ? in1 : in0)) {
                         const RowData &d = rd[(p + 1 - h + 2 * NS) % NS];
-                        double *row = ring[slot(1 - h)];
-                        const int x = x0 + cs;
-                        const double uN = ring[slot(-h)][x], uS = ring[slot(2 - h)][x];
-                        row[x] = gs_point_fast(cs ? d.r.y : d.r.x, cs ? d.x.y : d.x.x,
-                                               cs ? d.y.y : d.y.x, uN, row[x - 1], uS,
-                                               row[x + 1], c);
+                        double(*row)[LP] = ring[slot(1 - h)];
+                        const double uN = ring[slot(-h)][cs][pl], uS = ring[slot(2 - h)][cs][pl];
+                        // west / east neighbours are in the other plane:
+                        // even column 2c: odd 2c-1 (pl-1), 2c+1 (pl);
+                        // odd column 2c+1: even 2c (pl), 2c+2 (pl+1)
+                        const double uW = row[cs ^ 1][pl - 1 + cs];
+                        const double uE = row[cs ^ 1][pl + cs];
+                        row[cs][pl] = gs_point_fast(cs ? d.r.y : d.r.x, cs ? d.x.y : d.x.x,
+                                                    cs ? d.y.y : d.y.x, uN, uW, uS, uE, c);
                     }
                     __syncthreads();
                 }
@@ -589,34 +620,36 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
                 {
                     const int ro = s + 2 - S;
                     if (keep && ro >= a && ro < b)
-                        st2((uout + (long)ro * pitch) + c0, ld2(&ring[slot(2 - S)][x0]));
+                        st2s((uout + (long)ro * pitch) + c0,
+                            make_double2(ring[slot(2 - S)][0][pl], ring[slot(2 - S)][1][pl]));
                 }
                 // (4) residual stage on row s+1-S
                 if (C::REST || C::NORM) {
                     const int r = s + 1 - S;
                     const RowData &d = rd[(p + 1 - S + 2 * NS) % NS];
                     if (keep && r >= a && r < b && r >= 1 && r <= n - 1) {
-                        const double *rm = ring[slot(1 - S)], *rn_ = ring[slot(-S)],
-                                     *rs_ = ring[slot(2 - S)];
+                        const double(*rm)[LP] = ring[slot(1 - S)];
+                        const double(*rn_)[LP] = ring[slot(-S)];
+                        const double(*rs_)[LP] = ring[slot(2 - S)];
                         if (C::REST) {
                             // even-even points only: r even (static), c0 = 2J
                             if (((p + 1 - S) & 1) == 0 && in0 && c0 <= n - 2 && r <= n - 2) {
                                 const double res =
-                                    res_point(d.r.x, d.x.x, d.y.x, rm[x0], rn_[x0], rm[x0 - 1],
-                                              rs_[x0], rm[x0 + 1], c);
+                                    res_point(d.r.x, d.x.x, d.y.x, rm[0][pl], rn_[0][pl],
+                                              rm[1][pl - 1], rs_[0][pl], rm[1][pl], c);
                                 (rhsc + (long)(r >> 1) * pitchc)[c0 >> 1] = res;
                             }
                         } else {
                             if (in0) {
                                 const double res =
-                                    res_point(d.r.x, d.x.x, d.y.x, rm[x0], rn_[x0], rm[x0 - 1],
-                                              rs_[x0], rm[x0 + 1], c);
+                                    res_point(d.r.x, d.x.x, d.y.x, rm[0][pl], rn_[0][pl],
+                                              rm[1][pl - 1], rs_[0][pl], rm[1][pl], c);
                                 acc += res * res;
                             }
                             if (in1) {
                                 const double res =
-                                    res_point(d.r.y, d.x.y, d.y.y, rm[x0 + 1], rn_[x0 + 1],
-                                              rm[x0], rs_[x0 + 1], rm[x0 + 2], c);
+                                    res_point(d.r.y, d.x.y, d.y.y, rm[1][pl], rn_[1][pl],
+                                              rm[0][pl], rs_[1][pl], rm[0][pl + 1], c);
                                 acc += res * res;
                             }
                         }
@@ -637,6 +670,260 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
         __shared__ double red_lds[BLOCK / 64];
         const double tot = block_sum(acc, red_lds);
         if (l == 0) partials[blockIdx.x] = tot;
+    }
+}
+
+// k_wsmooth: the fused K-sweep pass of k_smooth as a WAVE-PRIVATE march.
+//
+// One workgroup = one wave of 64 lanes; lane l owns the column pair
+// (c0, c0+1), c0 = j0 - 2H + 2l.  Everything a stage needs lives in the
+// wave's own registers: a ring of u rows (double2 per lane), the rhs / v1 /
+// v2 ring (RowData per lane), and the west / east neighbour columns come
+// from the adjacent lanes by DPP wave shifts (v_mov_b32_dpp wave_shr:1 /
+// wave_shl:1).  No LDS and no barriers: the stage chain is a short run of
+// dependent fp64 VALU ops, and the two to three waves per SIMD overlap.
+//
+// Schedule (as k_smooth): at step s stage h (h = 0..S-1, S = 2K) updates
+// its colour in row s+1-h; the residual stage (RESTRICT / NORM) takes row
+// s+1-S; row s+2-S is final and stored.  u rows s-S .. s+3 are live (S+4 =
+// NR rows), rhs/v rows s+1-S .. s+3 (one spare slot, loaded two steps
+// ahead); NR is even and the step loop is unrolled NR times with its start
+// aligned to NR, so every ring index and every row parity is a compile-time
+// constant.
+//
+// The exact cone, halo lanes (H = ceil(E/2) pairs per side), clamped
+// unconditional loads, Markstein division and modes are those of k_smooth;
+// each exact value is computed from exactly the operands of the sequential
+// gs.cpp sweeps (bitwise).  The velocity terms enter as t = v*(h/2), which
+// is bitwise v*h/2.0 (scaling by 2^-1 is exact for these magnitudes), so a(v)
+// = rr*(nu - t) and b(v) = rr*(t + nu) exactly as gs.cpp:14-20.
+template <int K, int MODE>
+struct WCfg {
+    static constexpr bool ZERO = (MODE & 1) != 0;
+    static constexpr bool PROL = (MODE & 2) != 0;
+    static constexpr bool REST = (MODE & 4) != 0;
+    static constexpr bool NORM = (MODE & 8) != 0;
+    static constexpr int S = 2 * K;
+    static constexpr int E = S + ((REST || NORM) ? 1 : 0);
+    static constexpr int H = (E + 1) / 2;
+    static constexpr int NR = S + 4;   // u ring = rhs/v ring = unroll period (even)
+    static constexpr int W = 2 * (64 - 2 * H);
+};
+
+// 64-bit value of lane l-1 (shr) / l+1 (shl); edge lanes get garbage-free 0
+__device__ __forceinline__ double dpp_shr1(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x138, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x138, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double dpp_shl1(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x130, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x130, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// gs.cpp:130 / :75 with the velocity terms pre-scaled: t1 = v1*h/2, t2 = v2*h/2
+__device__ __forceinline__ double gs_point_t(double rhs, double t1, double t2, double uN,
+                                             double uW, double uS, double uE, const Coef &c) {
+    const double aa = c.rr * (c.nu - t2), bb = c.rr * (t2 + c.nu);
+    const double cc = c.rr * (c.nu - t1), dd = c.rr * (t1 + c.nu);
+    return div_diag(rhs - cc * uN - aa * uW - dd * uS - bb * uE, c);
+}
+__device__ __forceinline__ double res_point_t(double rhs, double t1, double t2, double u,
+                                              double uN, double uW, double uS, double uE,
+                                              const Coef &c) {
+    const double aa = c.rr * (c.nu - t2), bb = c.rr * (t2 + c.nu);
+    const double cc = c.rr * (c.nu - t1), dd = c.rr * (t1 + c.nu);
+    return rhs - (c.dgs * u + cc * uN + aa * uW + dd * uS + bb * uE);
+}
+
+template <int WPB, int K, int MODE>
+__global__ __launch_bounds__(64 * WPB) void k_wsmooth(
+    const double *__restrict__ uin, double *__restrict__ uout, const double *__restrict__ rhs,
+    const double *__restrict__ v1, const double *__restrict__ v2, const double *__restrict__ uc,
+    long pitchc, double *__restrict__ rhsc, double *__restrict__ partials, int n, long pitch,
+    int strips, long units_per_wg, Coef c, int ra, int rb, int lo, int hi) {
+    using C = WCfg<K, MODE>;
+    constexpr int S = C::S, E = C::E, H = C::H, NR = C::NR, W = C::W;
+    // WPB waves per workgroup march WPB adjacent strips over the same rows,
+    // independently (no barriers); their row loads are adjacent 1-KiB pieces
+    // of the same rows, issued at about the same time
+    const int l = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const int nrows = rb - ra;
+    const long total = (long)strips * nrows;   // strips = strip GROUPS of WPB
+    long start = (long)blockIdx.x * units_per_wg;
+    const long end = min(total, start + units_per_wg);
+    const int nc = n >> 1;
+    const double hh = c.h * 0.5;
+    double acc = 0.0;
+
+    while (start < end) {
+        const int strip = (int)(start / nrows);
+        const int a = ra + (int)(start % nrows);
+        const int b = (int)min((long)rb, (long)a + (end - start));
+        start += b - a;
+
+        const int j0 = (strip * WPB + wv) * W;
+        const int c0 = j0 - 2 * H + 2 * l;
+        const bool act = c0 >= 0 && c0 <= n;
+        const bool keep = act && l >= H && l < 64 - H;
+        const bool in0 = act && c0 >= 1 && c0 <= n - 1;
+        const bool in1 = act && c0 + 1 <= n - 1;
+
+        struct UPre {
+            double2 X;
+            double q00, q01, q10, q11;
+        };
+        UPre up[2];
+        up[0] = up[1] = UPre{make_double2(0.0, 0.0), 0.0, 0.0, 0.0, 0.0};
+        const int cl = min(max(c0, 0), (int)pitch - 2);
+        const int jl = cl >> 1;
+        const int j1 = (jl + 1 <= nc) ? 1 : 0;
+        auto load_u = [&](int R, UPre &u) {
+            if (C::ZERO) return;
+            const int Rc = min(max(R, lo), hi);
+            u.X = ld2((uin + (long)Rc * pitch) + cl);
+            if (C::PROL) {
+                const double *p0 = (uc + (long)(Rc >> 1) * pitchc) + jl;
+                const double *p1 = p0 + ((Rc & 1) ? pitchc : 0);
+                u.q00 = p0[0];
+                u.q01 = p0[j1];
+                u.q10 = p1[0];
+                u.q11 = p1[j1];
+            }
+        };
+        // u row R (+ prolongation) as it enters the ring
+        auto make_u = [&](int R, const UPre &u) {
+            double2 v = u.X;
+            if (C::ZERO) v = make_double2(0.0, 0.0);
+            if (C::PROL && act && R >= 0 && R <= n) {
+                double2 pr;
+                const double q01 = j1 ? u.q01 : 0.0;
+                const double q11 = j1 ? u.q11 : 0.0;
+                if (!(R & 1)) {
+                    pr.x = u.q00;
+                    pr.y = (u.q00 + q01) / 2;
+                } else {
+                    pr.x = (u.q00 + u.q10) / 2;
+                    pr.y = (u.q00 + u.q10 + q01 + q11) / 4;
+                }
+                v.x = v.x + pr.x;
+                v.y = v.y + pr.y;
+            }
+            return v;
+        };
+        // rhs and t = v*h/2 of row R
+        auto load_rv = [&](int R, RowData &d) {
+            const long o = (long)min(max(R, lo), hi) * pitch;
+            d.r = ld2((rhs + o) + cl);
+            const double2 x = ld2((v1 + o) + cl), y = ld2((v2 + o) + cl);
+            d.x = make_double2(x.x * hh, x.y * hh);
+            d.y = make_double2(y.x * hh, y.y * hh);
+        };
+
+        const int s_first = a - E;
+        const int s_last = b + E - 3;
+        int s = s_first >= 0 ? (s_first / NR) * NR : -(((-s_first) + NR - 1) / NR) * NR;
+        s = __builtin_amdgcn_readfirstlane(s);
+
+        double2 ur[NR];
+        RowData rd[NR];
+#pragma unroll
+        for (int q = 0; q < NR; ++q) {
+            ur[q] = make_double2(0.0, 0.0);
+            rd[q].r = rd[q].x = rd[q].y = make_double2(0.0, 0.0);
+        }
+        // prologue (s == 0 mod NR): u rows s..s+2 in the ring, s+3 / s+4 in
+        // flight (sets 1 / 0), rhs/v rows s+1, s+2 loaded
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            load_u(s + d, up[0]);
+            ur[d] = make_u(s + d, up[0]);
+        }
+        load_u(s + 3, up[1]);
+        load_u(s + 4, up[0]);
+        load_rv(s + 1, rd[1]);
+        load_rv(s + 2, rd[2]);
+
+        for (;;) {
+#pragma unroll
+            for (int p = 0; p < NR; ++p) {
+                // (1) u row s+3 enters the ring; its prefetch set takes row s+5
+                ur[(p + 3) % NR] = make_u(s + 3, up[(p + 1) & 1]);
+                load_u(s + 5, up[(p + 1) & 1]);
+                // (2) the S smoothing stages
+#pragma unroll
+                for (int h = 0; h < S; ++h) {
+                    const int r = s + 1 - h;
+                    const int iR = (p + 1 - h + 2 * NR) % NR;
+                    const int iN = (p - h + 2 * NR) % NR;
+                    const int iS = (p + 2 - h + 2 * NR) % NR;
+                    const int cs = ((p + 1 - h) & 1) ^ (h & 1);
+                    const RowData &d = rd[iR];
+                    const bool inr = r >= 1 && r <= n - 1;
+                    if (cs == 0) {
+                        const double uW = dpp_shr1(ur[iR].y);   // column c0-1
+                        if (inr && in0)
+                            ur[iR].x = gs_point_t(d.r.x, d.x.x, d.y.x, ur[iN].x, uW, ur[iS].x,
+                                                  ur[iR].y, c);
+                    } else {
+                        const double uE = dpp_shl1(ur[iR].x);   // column c0+2
+                        if (inr && in1)
+                            ur[iR].y = gs_point_t(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x,
+                                                  ur[iS].y, uE, c);
+                    }
+                }
+                // (3) row s+2-S is final
+                {
+                    const int ro = s + 2 - S;
+                    if (keep && ro >= a && ro < b)
+                        st2((uout + (long)ro * pitch) + c0, ur[(p + 2 - S + 2 * NR) % NR]);
+                }
+                // (4) residual stage on row s+1-S
+                if (C::REST || C::NORM) {
+                    const int r = s + 1 - S;
+                    const int iR = (p + 1 - S + 2 * NR) % NR;
+                    const int iN = (p - S + 2 * NR) % NR;
+                    const int iS = (p + 2 - S + 2 * NR) % NR;
+                    const RowData &d = rd[iR];
+                    const double uW = dpp_shr1(ur[iR].y);
+                    if (C::REST) {
+                        if (((p + 1 - S) & 1) == 0 && keep && r >= a && r < b && r >= 1 &&
+                            r <= n - 2 && in0 && c0 <= n - 2) {
+                            const double res = res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x,
+                                                           ur[iN].x, uW, ur[iS].x, ur[iR].y, c);
+                            (rhsc + (long)(r >> 1) * pitchc)[c0 >> 1] = res;
+                        }
+                    } else {
+                        const double uE = dpp_shl1(ur[iR].x);
+                        if (keep && r >= a && r < b && r >= 1 && r <= n - 1) {
+                            if (in0) {
+                                const double res = res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x,
+                                                               ur[iN].x, uW, ur[iS].x,
+                                                               ur[iR].y, c);
+                                acc += res * res;
+                            }
+                            if (in1) {
+                                const double res = res_point_t(d.r.y, d.x.y, d.y.y, ur[iR].y,
+                                                               ur[iN].y, ur[iR].x, ur[iS].y,
+                                                               uE, c);
+                                acc += res * res;
+                            }
+                        }
+                    }
+                }
+                // (5) rhs/v row s+3 into the slot of row s+3-NR (dead)
+                load_rv(s + 3, rd[(p + 3) % NR]);
+                if (++s > s_last) goto done;
+            }
+        }
+    done:;
+    }
+    if (C::NORM) {
+        const double tot = wave_sum(acc);
+        if (l == 0) partials[(long)blockIdx.x * WPB + wv] = tot;
     }
 }
 
@@ -1089,6 +1376,44 @@ static int smooth_inst(const SmoothArgs &A, hipStream_t s) {
     return (int)grid;
 }
 
+template <int WPB, int K, int MODE>
+static int smooth_winst(const SmoothArgs &A, hipStream_t s) {
+    constexpr int W = WCfg<K, MODE>::W;
+    static int slots = 0;   // resident workgroups of this instantiation
+    if (!slots) {
+        int dev = 0, cus = 0, per = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_wsmooth<WPB, K, MODE>,
+                                                           64 * WPB, 0);
+        slots = std::max(1, cus) * std::max(1, per);
+    }
+    const long n = A.n;
+    const int groups = (int)((n + 1 + (long)W * WPB - 1) / ((long)W * WPB));
+    const long total = (long)groups * (A.rb - A.ra);
+    long g = std::max<long>(1, std::min<long>(slots, total / 64));
+    g = std::min<long>(g, kNormBlocks / WPB);
+    const long upw = (total + g - 1) / g;
+    const unsigned grid = (unsigned)((total + upw - 1) / upw);
+    MGX_LAUNCH((k_wsmooth<WPB, K, MODE>), dim3(grid), dim3(64 * WPB), s, A.uin, A.uout, A.rhs,
+               A.v1, A.v2, A.uc, A.pitchc, A.rhsc, A.partials, (int)n, A.pitch, groups, upw,
+               A.c, A.ra, A.rb, A.lo, A.hi);
+    return (int)grid * WPB;   // NORM partials written
+}
+
+long g_march_kernel = -1;   // row march: 0 workgroup + LDS ring (k_smooth), 1 wave-private
+                            // k_wsmooth, 4 waves per workgroup, 2 the same, 1 wave
+
+static long march_kernel() {
+    if (g_march_kernel < 0) {
+        const char *e = getenv("MGX_MARCH_KERNEL");
+        g_march_kernel = e ? atol(e) : 1;
+    }
+    return g_march_kernel;
+}
+void set_march_kernel(long v) { g_march_kernel = v; }
+long get_march_kernel() { return march_kernel(); }
+
 long g_tile_max_n = -1;   // levels with n <= this use k_smooth_tile
 
 void set_tile_max_n(long v) { g_tile_max_n = v; }
@@ -1137,6 +1462,8 @@ static int smooth_block(const SmoothArgs &A, hipStream_t s) {
         if (g > 0) return g;
     }
     if (A.n >= 4096) {
+        if (march_kernel() == 1) return smooth_winst<4, K, MODE>(A, s);
+        if (march_kernel() == 2) return smooth_winst<1, K, MODE>(A, s);
         if (march_block() == 128) return smooth_inst<128, K, MODE>(A, s);
         return smooth_inst<256, K, MODE>(A, s);
     }
@@ -1167,6 +1494,13 @@ int launch_smooth(const SmoothArgs &A0, int sweeps, int mode, hipStream_t s) {
         A.hi = (int)A.n;
     }
     if (A.ra & 1) return -1;   // partitions start at even rows (parity, restriction)
+#ifdef MGX_PROBE_CLAMP
+    {   // experiment build only: every load from one row (L2-resident) -> the
+        // pass's compute + store time without the HBM read streams
+        A.lo = A.hi = 2;
+        A.uout = const_cast<double *>(A.uin);
+    }
+#endif
     int blocks = -1;
     switch (sweeps) {
         case 1: blocks = smooth_k<1>(A, mode, s); break;
@@ -1266,6 +1600,39 @@ void launch_coarse_solve(double *u, const double *rhs, const double *v1, const d
                          double *stats, hipStream_t s) {
     MGX_LAUNCH(k_coarse_solve, dim3(1), dim3(1024), s, u, rhs, v1, v2, (int)n, pitch, c, tol,
                maxit, zero_first ? 1 : 0, stats);
+}
+
+// ---------------------------------------------------------------- probes
+// Streaming-bandwidth probes (the practical HBM ceiling SURVEY 8d asks for
+// beside the 8 TB/s spec): `nin` double2 input streams and one output stream,
+// 16 B per lane, grid-stride, out[i] = sum of the inputs.  nin = 1 is a copy;
+// nin = 4 is the smoother's stream shape (u, rhs, v1, v2 in, u out).
+template <int NIN>
+__global__ __launch_bounds__(256) void k_stream(const double2 *__restrict__ a,
+                                                const double2 *__restrict__ b,
+                                                const double2 *__restrict__ c,
+                                                const double2 *__restrict__ d,
+                                                double2 *__restrict__ o, long n) {
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        double2 v = a[i];
+        if (NIN > 1) {
+            const double2 y = b[i], z = c[i], w = d[i];
+            v.x += y.x + z.x + w.x;
+            v.y += y.y + z.y + w.y;
+        }
+        o[i] = v;
+    }
+}
+
+void launch_stream(const double *a, const double *b, const double *c, const double *d,
+                   double *o, long n2, int nin, int grid, hipStream_t s) {
+    if (nin == 1)
+        MGX_LAUNCH(k_stream<1>, dim3(grid), dim3(256), s, (const double2 *)a, (const double2 *)b,
+                   (const double2 *)c, (const double2 *)d, (double2 *)o, n2);
+    else
+        MGX_LAUNCH(k_stream<4>, dim3(grid), dim3(256), s, (const double2 *)a, (const double2 *)b,
+                   (const double2 *)c, (const double2 *)d, (double2 *)o, n2);
 }
 
 }  // namespace mgx

@@ -664,8 +664,11 @@ int mgx_synchronize(mgx_ctx *c) {
 int mgx_profile_enable(mgx_ctx *c, int on) {
     if (!c) return fail(MGX_E_ARG, "null ctx");
     CHK(prof_flush(c));
-    c->prof = on != 0;
-    for (int i = 0; i < dist_nsub(c); ++i) CHK(mgx_profile_enable(dist_sub(c, i), on));
+    if (on < 0 || on > 2) return fail(MGX_E_ARG, "mgx_profile_enable: on must be 0, 1 or 2");
+    c->prof = on;
+    // the replicated levels of a partitioned context are never the finest
+    for (int i = 0; i < dist_nsub(c); ++i)
+        CHK(mgx_profile_enable(dist_sub(c, i), on == 1 ? 1 : 0));
     return MGX_OK;
 }
 int mgx_profile_reset(mgx_ctx *c) {
@@ -795,6 +798,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgx::set_march_block(value);
         return MGX_OK;
     }
+    if (!strcmp(key, "march_kernel")) {
+        if (value < 0 || value > 2) return fail(MGX_E_ARG, "march_kernel must be 0, 1 or 2");
+        mgx::set_march_kernel(value);
+        return MGX_OK;
+    }
     if (!strcmp(key, "dist_min_rows")) {
         if (value < 16 || (value & 1)) return fail(MGX_E_ARG, "dist_min_rows must be even, >= 16");
         mgxi::g_dist_min_rows = value;
@@ -812,9 +820,59 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
         *value = mgx::get_march_block();
         return MGX_OK;
     }
+    if (!strcmp(key, "march_kernel")) {
+        *value = mgx::get_march_kernel();
+        return MGX_OK;
+    }
     if (!strcmp(key, "dist_min_rows")) {
         *value = mgxi::g_dist_min_rows;
         return MGX_OK;
     }
     return fail(MGX_E_ARG, std::string("mgx_get_tuning: unknown key ") + key);
+}
+
+// Streaming-bandwidth probe (a measured ceiling beside the spec).
+extern "C" int mgx_stream_bandwidth(long bytes_per_stream, int nin, int reps, double *GBs) {
+    if (bytes_per_stream < (1 << 20) || (nin != 1 && nin != 4) || reps < 1 || !GBs)
+        return fail(MGX_E_ARG, "mgx_stream_bandwidth: bad args");
+    const long n2 = bytes_per_stream / 16;
+    const size_t bytes = (size_t)n2 * 16;
+    double *buf[5] = {};
+    hipStream_t s = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int rc = MGX_OK;
+    int dev = 0, cus = 0;
+    auto cleanup = [&]() {
+        for (double *b : buf) (void)hipFree(b);
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+        if (s) (void)hipStreamDestroy(s);
+    };
+    for (int k = 0; k <= nin; ++k)
+        if (hipMalloc(&buf[k], bytes) != hipSuccess ||
+            hipMemset(buf[k], 0, bytes) != hipSuccess) {
+            cleanup();
+            return fail(MGX_E_HIP, "mgx_stream_bandwidth: alloc");
+        }
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipStreamCreate(&s) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
+        hipEventCreate(&e1) != hipSuccess) {
+        cleanup();
+        return fail(MGX_E_HIP, "mgx_stream_bandwidth: stream/events");
+    }
+    const int grid = std::max(1, cus) * 8;   // 8 workgroups (32 waves) per CU
+    double *a = buf[0], *b = buf[nin > 1 ? 1 : 0], *c = buf[nin > 1 ? 2 : 0],
+           *d = buf[nin > 1 ? 3 : 0], *o = buf[nin];
+    mgx::launch_stream(a, b, c, d, o, n2, nin, grid, s);   // warm-up
+    (void)hipEventRecord(e0, s);
+    for (int r = 0; r < reps; ++r) mgx::launch_stream(a, b, c, d, o, n2, nin, grid, s);
+    (void)hipEventRecord(e1, s);
+    float ms = 0.f;
+    if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess)
+        rc = fail(MGX_E_HIP, "mgx_stream_bandwidth: timing");
+    else
+        *GBs = (double)bytes * (nin + 1) * reps / (ms * 1e-3) / 1e9;
+    cleanup();
+    return rc;
 }

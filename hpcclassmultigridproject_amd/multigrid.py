@@ -191,8 +191,9 @@ class Multigrid:
         return s.value
 
     # -- profiling (HIP events on the context stream)
-    def profile(self, on=True):
-        check(lib().mgx_profile_enable(self._h, 1 if on else 0))
+    def profile(self, on=True, finest_only=False):
+        """HIP events around launches: all levels, or the finest level only."""
+        check(lib().mgx_profile_enable(self._h, (2 if finest_only else 1) if on else 0))
 
     def profile_reset(self):
         check(lib().mgx_profile_reset(self._h))

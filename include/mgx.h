@@ -157,6 +157,8 @@ int mgx_synchronize(mgx_ctx *ctx);
  * fused smoothing pass as 2-D LDS tiles instead of the row march (default 2048;
  * env MGX_TILE_MAX_N).  "march_block": lanes per workgroup of the row march on
  * levels with n >= 4096, 128 or 256 (default 256; env MGX_MARCH_BLOCK).
+ * "march_kernel": row march on levels with n >= 4096: 1 wave-private
+ * registers + DPP (default), 0 workgroup with an LDS ring (env MGX_MARCH_KERNEL).
  * "dist_min_rows": partitioned solvers replicate every level whose row blocks
  * would be shorter than this (default 256, even, >= 16); read at creation. */
 int mgx_set_tuning(const char *key, long value);
@@ -172,6 +174,8 @@ int mgx_get_tuning(const char *key, long *value);
 #define MGX_K_HALO 6           /* halo exchange (multi-GPU) */
 #define MGX_K_PSMOOTH 7        /* prolongation + add fused into a smoothing pass */
 #define MGX_K_COUNT 8
+/* on: 0 off, 1 every launch, 2 finest-level launches only (two events per
+ * recorded launch; mode 2 keeps the overhead off the small levels). */
 int mgx_profile_enable(mgx_ctx *ctx, int on);
 int mgx_profile_reset(mgx_ctx *ctx);
 /* For kernel kind `kind` on level `level` (-1 = all levels): launches, summed
@@ -189,6 +193,12 @@ int mgx_profile_get(mgx_ctx *ctx, int kind, int level, long *launches, double *m
  * full grid, rhs, vcycle, mg_outer, step, run_cycles, residual_norm at level
  * 0); the per-level calls (gs, restrict, prolong_add, download_level) return
  * MGX_E_ARG.  Needs smoother 0, nsmooth >= 1, world a power of two. */
+/* Measured streaming bandwidth (GB/s, read + write bytes) of a 16-B-per-lane
+ * grid-stride kernel with `nin` input streams (1: copy; 4: the smoother's
+ * shape, 4 in + 1 out) of `bytes_per_stream` each, `reps` launches timed with
+ * HIP events: the practical HBM ceiling reported beside the 8 TB/s spec. */
+int mgx_stream_bandwidth(long bytes_per_stream, int nin, int reps, double *GBs);
+
 #define MGX_UNIQUE_ID_BYTES 128
 /* RCCL unique id (128 bytes) made on one rank and shared with the others. */
 int mgx_dist_unique_id(void *id128);

@@ -14,6 +14,8 @@ CGROUPS=(
   "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum"
   "GRBM_GUI_ACTIVE GRBM_COUNT"
 )
+# PMC_GROUPS="grp1;grp2" overrides the list
+if [ -n "$PMC_GROUPS" ]; then IFS=';' read -r -a CGROUPS <<< "$PMC_GROUPS"; fi
 for grp in "${CGROUPS[@]}"; do
   tag=$(echo $grp | cut -d' ' -f1)
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d "$OUT/$tag" -o run --output-format csv -- python3 tools/pmc_vcycle.py "$@" > "$OUT/$tag.log" 2>&1 || echo "group $tag failed"
