@@ -39,10 +39,23 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s HBM3E
-# (kind, level) -> kernel instance of the default config, for the PMC traffic
-# summary committed under profiles/ (tools/pmc_collect.sh, tools/pmc_summary.py)
-KERNEL_IDS = {(0, 0): "mgx::k_smooth<256, 3, 4> grid=196608",
-              (7, 0): "mgx::k_smooth<256, 3, 10> grid=196608"}
+# (kind, level) -> kernel (template instance) of the default config, for the
+# PMC traffic summary committed under profiles/ (tools/profile_round.sh)
+KERNEL_IDS = {(8, 0): "mgx::k_xsmooth<4, 3>",
+              (0, 0): "mgx::k_wsmooth<4, 3, 4>",
+              (7, 0): "mgx::k_wsmooth<4, 3, 10>"}
+TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r1_hbm_traffic.json")
+
+
+def lookup_traffic(kname):
+    """HBM bytes per dispatch of the finest-level instance (largest grid) of kname."""
+    if not os.path.exists(TRAFFIC_JSON):
+        return None, None
+    best = None
+    for key, v in json.load(open(TRAFFIC_JSON))["kernels"].items():
+        if key.split(" grid=")[0] == kname and (best is None or v["hbm_bytes"] > best[1]):
+            best = (key, v["hbm_bytes"])
+    return best if best else (None, None)
 
 
 def parse():
@@ -206,10 +219,7 @@ def main():
                                                 args.fuse) == (16384, 9, 3, 0, 3) else None
         traffic = None
         if kname:
-            prof = os.path.join(ROOT, "profiles", "r1_hbm_traffic.json")
-            if os.path.exists(prof):
-                t = json.load(open(prof))["kernels"].get(kname)
-                traffic = t["hbm_bytes"] if t else None
+            kname, traffic = lookup_traffic(kname)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": f"{_lib.KERNEL_NAMES[kind]} level {lvl}"

@@ -10,16 +10,18 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmgx.so")
+# MGX_LIB: an alternative build of the same library (A/B experiments)
+LIB_PATH = os.environ.get("MGX_LIB", os.path.join(HERE, "libmgx.so"))
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "mgx.h")
 
 MGX_OK, MGX_E_ARG, MGX_E_HIP, MGX_E_RCCL, MGX_E_NOCONV = 0, 1, 2, 3, 4
 TOWER_REFERENCE, TOWER_CORRECT = 0, 1
 UNIQUE_ID_BYTES = 128   # MGX_UNIQUE_ID_BYTES (ncclUniqueId)
-K_GS, K_RESTRICT, K_PROLONG, K_RESNORM, K_COARSE, K_RHS, K_HALO, K_PSMOOTH = range(8)
+K_GS, K_RESTRICT, K_PROLONG, K_RESNORM, K_COARSE, K_RHS, K_HALO, K_PSMOOTH, K_XSMOOTH = range(9)
 KERNEL_NAMES = {K_GS: "gs_sweep", K_RESTRICT: "residual_restrict", K_PROLONG: "prolong_add",
                 K_RESNORM: "residual_norm", K_COARSE: "coarse_solve", K_RHS: "compute_rhs",
-                K_HALO: "halo_exchange", K_PSMOOTH: "prolong_smooth"}
+                K_HALO: "halo_exchange", K_PSMOOTH: "prolong_smooth",
+                K_XSMOOTH: "cross_cycle_smooth"}
 
 
 class MGXError(RuntimeError):

@@ -29,9 +29,14 @@ int check_launch(const char *what);
 
 struct Level {
     long n = 0, pitch = 0;
-    double *u[2] = {nullptr, nullptr};
+    double *u[3] = {nullptr, nullptr, nullptr};   // u[2]: finest level, cross-cycle pass
     int cur = 0;
     bool zero = false;   // u is logically all zeros (multigrid.cpp:77), not yet written
+    // finest level only: index of the buffer holding the NEXT cycle's
+    // pre-smoothed u (written by the cross-cycle pass, with rhs[1] restricted
+    // from it and u[1] flagged zero), or -1
+    int spec = -1;
+    int nxt() const { return cur == 0 ? 1 : 0; }   // ping-pong partner of cur
     double *rhs = nullptr, *v1 = nullptr, *v2 = nullptr;
     mgx::Coef coef{};
     double M() const { return double(n + 1) * double(n + 1); }

@@ -77,6 +77,24 @@ struct SmoothArgs {
     int ra = 0, rb = -1, lo = 0, hi = -1;
 };
 int launch_smooth(const SmoothArgs &a, int sweeps, int mode, hipStream_t s);
+
+// Cross-cycle fused finest-level pass (k_xsmooth): post-smoothing of cycle k
+// (u_in + P(uc), `sweeps` sweeps, residual norm -> *norm_out as sqrt) into
+// upost, and the pre-smoothing of cycle k+1 (`sweeps` sweeps, residual
+// restricted into rhsc) into upre.  sweeps 2 or 3; returns the partials count
+// or -1.  Whole level only (no row partition).
+struct XArgs {
+    const double *uin = nullptr;
+    double *upost = nullptr, *upre = nullptr;
+    const double *rhs = nullptr, *v1 = nullptr, *v2 = nullptr;
+    const double *uc = nullptr;
+    long pitchc = 0;
+    double *rhsc = nullptr;
+    double *partials = nullptr, *norm_out = nullptr;
+    long n = 0, pitch = 0;
+    Coef c{};
+};
+int launch_xsmooth(const XArgs &a, int sweeps, hipStream_t s);
 // Levels with n <= tile_max_n use the 2-D tile form of the fused pass (small
 // levels: latency bound), larger ones the row march.  Default 2048, or the
 // MGX_TILE_MAX_N environment variable.

@@ -927,6 +927,278 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
     }
 }
 
+// k_xsmooth: the finest level's post-smoothing of V-cycle k FUSED with the
+// pre-smoothing of V-cycle k+1 (software pipelining across cycles): in
+// mg_outer the two are consecutive sweeps of level 0 with only the residual
+// norm between them (multigrid.cpp:83-88 of cycle k, :112-113, :69-75 of
+// cycle k+1), so one HBM pass can do both, reading rhs / v1 / v2 / u once.
+//
+// Workgroup = WPB pairs of waves on WPB adjacent strips.  In each pair, wave
+// A runs the k_wsmooth march of the post-smoothing (prolongation + add on
+// load, K sweeps, residual-norm partials) and wave B, D = S+2 rows behind,
+// the march of the next pre-smoothing (K sweeps, residual restricted to the
+// coarse rhs).  A hands B each finished u row and each rhs / v row through a
+// small LDS ring (one lane to the same lane: no bank conflicts); one barrier
+// per step keeps the pair D rows apart.  Register footprint per wave = that
+// of one K-sweep march.  A also stores u_post (the solution after cycle k,
+// which mg_outer returns if cycle k converged); B stores u_pre (cycle k+1
+// after its pre-smoothing).  Exactness: B's output strip needs A's output
+// on a cone EB = S+1 wider, A's on S more: H = ceil((S+EB)/2) halo pairs.
+template <int K>
+struct XCfg {
+    static constexpr int S = 2 * K;
+    static constexpr int EB = S + 1;             // B: stages + restriction residual
+    static constexpr int EA = S + 1;             // A: stages + norm residual
+    static constexpr int H = (S + EB + 1) / 2;   // halo pairs per side
+    static constexpr int NR = S + 4;             // register rings / unroll period
+    static constexpr int W = 2 * (64 - 2 * H);
+    static constexpr int D = S + 2;              // B's lag in rows
+    static constexpr int NU = 4, NRD = 8;        // LDS hand-off rings (rows)
+};
+
+template <int WPB, int K>
+__global__ __launch_bounds__(128 * WPB) void k_xsmooth(
+    const double *__restrict__ uin, double *__restrict__ upost, double *__restrict__ upre,
+    const double *__restrict__ rhs, const double *__restrict__ v1, const double *__restrict__ v2,
+    const double *__restrict__ uc, long pitchc, double *__restrict__ rhsc,
+    double *__restrict__ partials, int n, long pitch, int groups, long units_per_wg, Coef c,
+    int lo, int hi) {
+    using X = XCfg<K>;
+    constexpr int S = X::S, H = X::H, NR = X::NR, W = X::W, D = X::D, NU = X::NU,
+                  NRD = X::NRD, EA = X::EA, EB = X::EB;
+    __shared__ double2 uring[WPB][NU][64];
+    // rhs / t1 / t2 planes: each hand-off access is 16 B per lane, unit stride
+    __shared__ double2 rdring[WPB][NRD][3][64];
+
+    const int l = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const bool isA = wv < WPB;   // wave-uniform role
+    const int pr = isA ? wv : wv - WPB;
+    const int nrows = n + 1;
+    const long total = (long)groups * nrows;
+    long start = (long)blockIdx.x * units_per_wg;
+    const long end = min(total, start + units_per_wg);
+    const int nc = n >> 1;
+    const double hh = c.h * 0.5;
+    double acc = 0.0;
+
+    while (start < end) {
+        const int grp = (int)(start / nrows);
+        const int a = (int)(start % nrows);
+        const int b = (int)min((long)nrows, (long)a + (end - start));
+        start += b - a;
+
+        const int j0 = (grp * WPB + pr) * W;
+        const int c0 = j0 - 2 * H + 2 * l;
+        const bool act = c0 >= 0 && c0 <= n;
+        const bool keep = act && l >= H && l < 64 - H;
+        const bool in0 = act && c0 >= 1 && c0 <= n - 1;
+        const bool in1 = act && c0 + 1 <= n - 1;
+        const int cl = min(max(c0, 0), (int)pitch - 2);
+        const int jl = cl >> 1;
+        const int j1 = (jl + 1 <= nc) ? 1 : 0;
+
+        struct UPre {
+            double2 X;
+            double q00, q01, q10, q11;
+        };
+        UPre up[2];
+        up[0] = up[1] = UPre{make_double2(0.0, 0.0), 0.0, 0.0, 0.0, 0.0};
+        auto load_u = [&](int R, UPre &u) {   // A: u row R + its coarse parents
+            const int Rc = min(max(R, lo), hi);
+            u.X = ld2((uin + (long)Rc * pitch) + cl);
+            const double *p0 = (uc + (long)(Rc >> 1) * pitchc) + jl;
+            const double *p1 = p0 + ((Rc & 1) ? pitchc : 0);
+            u.q00 = p0[0];
+            u.q01 = p0[j1];
+            u.q10 = p1[0];
+            u.q11 = p1[j1];
+        };
+        auto make_u = [&](int R, const UPre &u) {   // + prolongation (gs.cpp:238-265)
+            double2 v = u.X;
+            if (act && R >= 0 && R <= n) {
+                double2 pv;
+                const double q01 = j1 ? u.q01 : 0.0;
+                const double q11 = j1 ? u.q11 : 0.0;
+                if (!(R & 1)) {
+                    pv.x = u.q00;
+                    pv.y = (u.q00 + q01) / 2;
+                } else {
+                    pv.x = (u.q00 + u.q10) / 2;
+                    pv.y = (u.q00 + u.q10 + q01 + q11) / 4;
+                }
+                v.x = v.x + pv.x;
+                v.y = v.y + pv.y;
+            }
+            return v;
+        };
+        auto load_rv = [&](int R, RowData &d) {
+            const long o = (long)min(max(R, lo), hi) * pitch;
+            d.r = ld2((rhs + o) + cl);
+            const double2 x = ld2((v1 + o) + cl), y = ld2((v2 + o) + cl);
+            d.x = make_double2(x.x * hh, x.y * hh);
+            d.y = make_double2(y.x * hh, y.y * hh);
+        };
+
+        // A's first step (aligned to NR so ring indices and parities are
+        // static); B runs D steps behind; the last iteration is B's last step
+        int s0 = a - EB - EA;
+        s0 = s0 >= 0 ? (s0 / NR) * NR : -(((-s0) + NR - 1) / NR) * NR;
+        s0 = __builtin_amdgcn_readfirstlane(s0);
+        const int iters = (b + EB - 3) + D - s0 + 1;
+
+        double2 ur[NR];
+        RowData rd[NR];
+#pragma unroll
+        for (int q = 0; q < NR; ++q) {
+            ur[q] = make_double2(0.0, 0.0);
+            rd[q].r = rd[q].x = rd[q].y = make_double2(0.0, 0.0);
+        }
+        if (isA) {
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                load_u(s0 + d, up[0]);
+                ur[d] = make_u(s0 + d, up[0]);
+            }
+            load_u(s0 + 3, up[1]);
+            load_u(s0 + 4, up[0]);
+            load_rv(s0 + 1, rd[1]);
+            load_rv(s0 + 2, rd[2]);
+        }
+
+        int it = 0;
+        for (;;) {
+#pragma unroll
+            for (int p = 0; p < NR; ++p) {
+                if (isA) {
+                    const int s = s0 + it;
+                    ur[(p + 3) % NR] = make_u(s + 3, up[(p + 1) & 1]);
+                    load_u(s + 5, up[(p + 1) & 1]);
+#pragma unroll
+                    for (int h = 0; h < S; ++h) {
+                        const int r = s + 1 - h;
+                        const int iR = (p + 1 - h + 2 * NR) % NR;
+                        const int iN = (p - h + 2 * NR) % NR;
+                        const int iS = (p + 2 - h + 2 * NR) % NR;
+                        const int cs = ((p + 1 - h) & 1) ^ (h & 1);
+                        const RowData &d = rd[iR];
+                        const bool inr = r >= 1 && r <= n - 1;
+                        if (cs == 0) {
+                            const double uW = dpp_shr1(ur[iR].y);
+                            if (inr && in0)
+                                ur[iR].x = gs_point_t(d.r.x, d.x.x, d.y.x, ur[iN].x, uW,
+                                                      ur[iS].x, ur[iR].y, c);
+                        } else {
+                            const double uE = dpp_shl1(ur[iR].x);
+                            if (inr && in1)
+                                ur[iR].y = gs_point_t(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x,
+                                                      ur[iS].y, uE, c);
+                        }
+                    }
+                    // hand-off: rhs/v row s+1 (first used above), final u row s+2-S
+                    {
+                        const RowData &dh = rd[(p + 1) % NR];
+                        double2(*slot)[64] = rdring[pr][(s + 1) & (NRD - 1)];
+                        slot[0][l] = dh.r;
+                        slot[1][l] = dh.x;
+                        slot[2][l] = dh.y;
+                    }
+                    {
+                        const int ro = s + 2 - S;
+                        const double2 uf = ur[(p + 2 - S + 2 * NR) % NR];
+                        uring[pr][ro & (NU - 1)][l] = uf;
+                        if (keep && ro >= a && ro < b) st2((upost + (long)ro * pitch) + c0, uf);
+                    }
+                    load_rv(s + 3, rd[(p + 3) % NR]);
+                } else {
+                    const int s = s0 + it - D;   // B's ring phase q = p - D (mod NR)
+                    constexpr int dq = ((D % NR) + NR) % NR;
+                    const int q = (p - dq + NR) % NR;   // compile-time after unrolling
+                    // u row s+3 (A finished it last step) and rhs/v row s+3
+                    ur[(q + 3) % NR] = uring[pr][(s + 3) & (NU - 1)][l];
+                    {
+                        double2(*slot)[64] = rdring[pr][(s + 3) & (NRD - 1)];
+                        rd[(q + 3) % NR].r = slot[0][l];
+                        rd[(q + 3) % NR].x = slot[1][l];
+                        rd[(q + 3) % NR].y = slot[2][l];
+                    }
+                    // residual norm of u_post (multigrid.cpp:112-113) on row s+2:
+                    // rows s+1..s+3 are still untouched u_post here
+                    {
+                        const int r = s + 2;
+                        const int iR = (q + 2) % NR, iN = (q + 1) % NR, iS = (q + 3) % NR;
+                        const RowData &d = rd[iR];
+                        const double uW = dpp_shr1(ur[iR].y);
+                        const double uE = dpp_shl1(ur[iR].x);
+                        if (keep && r >= a && r < b && r >= 1 && r <= n - 1) {
+                            if (in0) {
+                                const double res = res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x,
+                                                               ur[iN].x, uW, ur[iS].x,
+                                                               ur[iR].y, c);
+                                acc += res * res;
+                            }
+                            if (in1) {
+                                const double res = res_point_t(d.r.y, d.x.y, d.y.y, ur[iR].y,
+                                                               ur[iN].y, ur[iR].x, ur[iS].y,
+                                                               uE, c);
+                                acc += res * res;
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int h = 0; h < S; ++h) {
+                        const int r = s + 1 - h;
+                        const int iR = (q + 1 - h + 2 * NR) % NR;
+                        const int iN = (q - h + 2 * NR) % NR;
+                        const int iS = (q + 2 - h + 2 * NR) % NR;
+                        const int cs = ((q + 1 - h) & 1) ^ (h & 1);
+                        const RowData &d = rd[iR];
+                        const bool inr = r >= 1 && r <= n - 1;
+                        if (cs == 0) {
+                            const double uW = dpp_shr1(ur[iR].y);
+                            if (inr && in0)
+                                ur[iR].x = gs_point_t(d.r.x, d.x.x, d.y.x, ur[iN].x, uW,
+                                                      ur[iS].x, ur[iR].y, c);
+                        } else {
+                            const double uE = dpp_shl1(ur[iR].x);
+                            if (inr && in1)
+                                ur[iR].y = gs_point_t(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x,
+                                                      ur[iS].y, uE, c);
+                        }
+                    }
+                    {
+                        const int ro = s + 2 - S;
+                        if (keep && ro >= a && ro < b)
+                            st2((upre + (long)ro * pitch) + c0,
+                                ur[(q + 2 - S + 2 * NR) % NR]);
+                    }
+                    {   // residual -> coarse rhs at the even-even points (:73-75)
+                        const int r = s + 1 - S;
+                        const int iR = (q + 1 - S + 2 * NR) % NR;
+                        const int iN = (q - S + 2 * NR) % NR;
+                        const int iS = (q + 2 - S + 2 * NR) % NR;
+                        const RowData &d = rd[iR];
+                        const double uW = dpp_shr1(ur[iR].y);
+                        if (((q + 1 - S) & 1) == 0 && keep && r >= a && r < b && r >= 1 &&
+                            r <= n - 2 && in0 && c0 <= n - 2) {
+                            const double res = res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x,
+                                                           ur[iN].x, uW, ur[iS].x, ur[iR].y, c);
+                            (rhsc + (long)(r >> 1) * pitchc)[c0 >> 1] = res;
+                        }
+                    }
+                }
+                __syncthreads();
+                if (++it == iters) goto done;
+            }
+        }
+    done:;
+    }
+    if (!isA) {
+        const double tot = wave_sum(acc);
+        if (l == 0) partials[(long)blockIdx.x * WPB + pr] = tot;
+    }
+}
+
 // k_smooth_tile: the same fused pass (K sweeps + optional prolong / restrict
 // / norm) for SMALL levels, where the serial row march of k_smooth is latency
 // bound.  A workgroup owns a TR x TC output tile and loads it with an EH-wide
@@ -1399,6 +1671,51 @@ static int smooth_winst(const SmoothArgs &A, hipStream_t s) {
                A.v1, A.v2, A.uc, A.pitchc, A.rhsc, A.partials, (int)n, A.pitch, groups, upw,
                A.c, A.ra, A.rb, A.lo, A.hi);
     return (int)grid * WPB;   // NORM partials written
+}
+
+template <int WPB, int K>
+static int xsmooth_inst(const XArgs &A, hipStream_t s) {
+    constexpr int W = XCfg<K>::W;
+    static int slots = 0;
+    if (!slots) {
+        int dev = 0, cus = 0, per = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_xsmooth<WPB, K>, 128 * WPB,
+                                                           0);
+        slots = std::max(1, cus) * std::max(1, per);
+    }
+    const long n = A.n;
+    const int groups = (int)((n + 1 + (long)W * WPB - 1) / ((long)W * WPB));
+    const long total = (long)groups * (n + 1);
+    long g = std::max<long>(1, std::min<long>(slots, total / 64));
+    g = std::min<long>(g, kNormBlocks / WPB);
+    const long upw = (total + g - 1) / g;
+    const unsigned grid = (unsigned)((total + upw - 1) / upw);
+    int lo = 0, hi = (int)n;
+#ifdef MGX_PROBE_CLAMP
+    lo = hi = 2;   // experiment build only: every load from one row (L2-resident)
+#endif
+    MGX_LAUNCH((k_xsmooth<WPB, K>), dim3(grid), dim3(128 * WPB), s, A.uin, A.upost, A.upre,
+               A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, A.partials, (int)n, A.pitch, groups,
+               upw, A.c, lo, hi);
+    return (int)grid * WPB;
+}
+
+int launch_xsmooth(const XArgs &A, int sweeps, hipStream_t s) {
+    int blocks = -1;
+    // 4 strip pairs per workgroup (one workgroup of 8 waves per CU): adjacent
+    // 1-KiB row pieces of four strips per load (measured: 4.05 ms vs 4.13 ms
+    // with 2 pairs, N=16384)
+    switch (sweeps) {
+        case 2: blocks = xsmooth_inst<4, 2>(A, s); break;
+        case 3: blocks = xsmooth_inst<4, 3>(A, s); break;
+        default: return -1;
+    }
+    if (blocks > 0)
+        MGX_LAUNCH(k_norm_final, dim3(1), dim3(kFinalThreads), s, (const double *)A.partials,
+                   blocks, A.norm_out, 1);
+    return blocks;
 }
 
 long g_march_kernel = -1;   // row march: 0 workgroup + LDS ring (k_smooth), 1 wave-private

@@ -22,6 +22,18 @@ namespace mgxi {
 
 thread_local std::string g_err;
 
+// Cross-cycle fusion of the finest level (k_xsmooth) on levels this large
+// (the row-march regime); tuning key "cross_cycle" turns it off.
+constexpr long kCrossMinN = 4096;
+long g_cross_cycle = -1;
+static bool cross_cycle_on() {
+    if (g_cross_cycle < 0) {
+        const char *e = getenv("MGX_CROSS_CYCLE");
+        g_cross_cycle = e ? atol(e) : 1;
+    }
+    return g_cross_cycle != 0;
+}
+
 int fail(int code, const std::string &msg) {
     g_err = msg;
     return code;
@@ -99,7 +111,7 @@ int op_smooth(mgx_ctx *c, int l, int sweeps, bool prolong, bool restrict_, bool 
             if (nm) mode |= mgx::kModeNorm;
             mgx::SmoothArgs A{};
             A.uin = L.u[L.cur];
-            A.uout = L.u[L.cur ^ 1];
+            A.uout = L.u[L.nxt()];
             A.rhs = L.rhs;
             A.v1 = L.v1;
             A.v2 = L.v2;
@@ -125,7 +137,7 @@ int op_smooth(mgx_ctx *c, int l, int sweeps, bool prolong, bool restrict_, bool 
             int blocks = 0;
             CHK(launch(c, kind, l, bytes, [&] { blocks = mgx::launch_smooth(A, k, mode, c->stream); }));
             if (blocks < 0) return fail(MGX_E_ARG, "launch_smooth: unsupported sweeps/mode");
-            L.cur ^= 1;
+            L.cur = L.nxt();
             L.zero = false;
             if (rs) c->lv[l + 1].zero = true;
             if (nm && fused_norm) *fused_norm = true;
@@ -139,10 +151,10 @@ int op_smooth(mgx_ctx *c, int l, int sweeps, bool prolong, bool restrict_, bool 
         if (c->opt.smoother == 2) {
             const bool z = L.zero;
             CHK(launch(c, MGX_K_GS, l, 40.0 * L.M(), [&] {
-                mgx::launch_gs_sweep(L.u[L.cur], L.u[L.cur ^ 1], L.rhs, L.v1, L.v2, L.n, L.pitch,
+                mgx::launch_gs_sweep(L.u[L.cur], L.u[L.nxt()], L.rhs, L.v1, L.v2, L.n, L.pitch,
                                      L.coef, z, c->stream);
             }));
-            L.cur ^= 1;
+            L.cur = L.nxt();
             L.zero = false;
         } else {
             CHK(materialize(c, l));
@@ -232,10 +244,83 @@ int op_coarse(mgx_ctx *c, int l) {
     return MGX_OK;
 }
 
+// Can level 0 run the cross-cycle pass (post of cycle k + pre of cycle k+1)?
+static bool cross_ok(mgx_ctx *c) {
+    const Level &L = c->lv[0];
+    return cross_cycle_on() && !c->dist && c->L > 1 && L.u[2] && c->opt.smoother == 0 &&
+           c->opt.shape == 1 && (c->opt.nsmooth == 2 || c->opt.nsmooth == 3) &&
+           c->opt.fuse >= c->opt.nsmooth;
+}
+
+// The speculative next-cycle state is only valid while nothing but V-cycles
+// touches the levels; every other mutating entry point drops it.
+void drop_spec(mgx_ctx *c) {
+    if (!c->lv.empty()) c->lv[0].spec = -1;
+}
+
+// k_xsmooth on level 0: u_post (cycle k, returned by mg_outer if it stops
+// here) into one free buffer, u_pre (cycle k+1's pre-smoothing) into the
+// other, the residual of u_post -> c->dscal[0], the restriction of u_pre's
+// residual -> rhs[1] (u[1] flagged zero for cycle k+1).
+static int op_cross(mgx_ctx *c) {
+    Level &L = c->lv[0], &Cl = c->lv[1];
+    CHK(materialize(c, 1));
+    int P = -1, Q = -1;
+    for (int i = 0; i < 3; ++i)
+        if (i != L.cur) (P < 0 ? P : Q) = i;
+    mgx::XArgs A;
+    A.uin = L.U();
+    A.upost = L.u[P];
+    A.upre = L.u[Q];
+    A.rhs = L.rhs;
+    A.v1 = L.v1;
+    A.v2 = L.v2;
+    A.uc = Cl.U();
+    A.pitchc = Cl.pitch;
+    A.rhsc = Cl.rhs;
+    A.partials = c->partials;
+    A.norm_out = c->dscal;
+    A.n = L.n;
+    A.pitch = L.pitch;
+    A.c = L.coef;
+    const int k = c->opt.nsmooth;
+    // algorithmic bytes: prolong+add, k sweeps, residual+norm (post of cycle
+    // k) + k sweeps, residual+restriction (pre of cycle k+1), SURVEY 8d
+    const double bytes = (32.0 + 40.0 * k + 48.0) * L.M() + 8.0 * Cl.M() +
+                         (40.0 * k + 40.0) * L.M() + 24.0 * Cl.M();
+    int blocks = 0;
+    CHK(launch(c, MGX_K_XSMOOTH, 0, bytes,
+               [&] { blocks = mgx::launch_xsmooth(A, k, c->stream); }));
+    if (blocks < 0) return fail(MGX_E_ARG, "launch_xsmooth: unsupported sweeps");
+    L.cur = P;
+    L.spec = Q;
+    L.zero = false;
+    Cl.zero = true;
+    return MGX_OK;
+}
+
 // mg_inner (multigrid.cpp:17-92).  If norm != nullptr (finest level only) the
 // residual norm after the cycle (multigrid.cpp:112-113) is produced too, fused
 // into the last post-smoothing pass when possible.
+//
+// Finest level with a norm (mg_outer's cycles): the post-smoothing of this
+// cycle and the pre-smoothing of the NEXT one are one k_xsmooth pass, so a
+// cycle is [pre (first cycle only) | coarse levels | cross pass]; a cycle that
+// follows one starts from the speculative state the cross pass left.
 int op_vcycle(mgx_ctx *c, int l, double *norm) {
+    if (l == 0 && norm && cross_ok(c)) {
+        Level &L = c->lv[0];
+        if (L.spec >= 0) {   // pre-smoothing + restriction already done
+            L.cur = L.spec;
+            L.spec = -1;
+        } else {
+            CHK(op_smooth(c, 0, c->opt.nsmooth, false, /*restrict=*/true, false, nullptr));
+        }
+        CHK(op_vcycle(c, 1));
+        CHK(op_cross(c));
+        return read_norm(c, norm);
+    }
+    if (l == 0) drop_spec(c);
     bool have_norm = false;
     for (int sh = 0; sh < c->opt.shape; ++sh) {
         const bool last = sh == c->opt.shape - 1;
@@ -258,6 +343,7 @@ int op_vcycle(mgx_ctx *c, int l, double *norm) {
 }
 
 int op_rhs(mgx_ctx *c) {
+    drop_spec(c);
     CHK(materialize(c, 0));
     Level &L = c->lv[0];
     return launch(c, MGX_K_RHS, 0, 32.0 * L.M(), [&] {
@@ -337,6 +423,7 @@ void free_ctx(mgx_ctx *c) {
     for (auto &L : c->lv) {
         (void)hipFree(L.u[0]);
         (void)hipFree(L.u[1]);
+        (void)hipFree(L.u[2]);
         (void)hipFree(L.rhs);
         (void)hipFree(L.v1);
         (void)hipFree(L.v2);
@@ -493,6 +580,12 @@ int mgxi::create_ctx(mgx_ctx **out, long n, int maxlvl, double dt, double nu,
                 return bail(fail(MGX_E_HIP, "hipMemset"));
         }
     }
+    if (maxlvl > 1 && n >= kCrossMinN) {   // third finest-level buffer: cross-cycle pass
+        Level &L = c->lv[0];
+        const size_t bytes = sizeof(double) * L.pitch * (L.n + 1);
+        if (hipMalloc(&L.u[2], bytes) != hipSuccess)
+            return bail(fail(MGX_E_HIP, "hipMalloc (level tower): out of device memory"));
+    }
     const size_t flat = sizeof(double) * (n + 1) * (n + 1);
     if (hipMalloc(&c->partials, sizeof(double) * mgx::norm_partials_size()) != hipSuccess ||
         hipMalloc(&c->dscal, sizeof(double) * 8) != hipSuccess ||
@@ -530,6 +623,7 @@ int mgxi::upload_ctx(mgx_ctx *c, const double *u0, const double *v1, const doubl
     const size_t row = (c->N + 1) * sizeof(double);
     L.cur = 0;
     L.zero = false;
+    L.spec = -1;
     const double *src[3] = {u0, v1, v2};
     double *dst[3] = {L.u[0], L.v1, L.v2};
     for (int k = 0; k < 3; ++k)
@@ -594,6 +688,7 @@ int mgx_rhs(mgx_ctx *c) {
 int mgx_gs(mgx_ctx *c, int level, int sweeps) {
     if (!c || level < 0 || level >= c->L || sweeps < 0) return fail(MGX_E_ARG, "mgx_gs: bad args");
     if (c->dist) return no_dist(c, "mgx_gs");
+    drop_spec(c);
     return op_gs(c, level, sweeps);
 }
 int mgx_residual_norm(mgx_ctx *c, int level, double *norm) {
@@ -607,11 +702,13 @@ int mgx_residual_norm(mgx_ctx *c, int level, double *norm) {
 int mgx_restrict(mgx_ctx *c, int level) {
     if (!c || level < 0 || level >= c->L - 1) return fail(MGX_E_ARG, "mgx_restrict: bad level");
     if (c->dist) return no_dist(c, "mgx_restrict");
+    drop_spec(c);
     return op_restrict(c, level);
 }
 int mgx_prolong_add(mgx_ctx *c, int level) {
     if (!c || level < 0 || level >= c->L - 1) return fail(MGX_E_ARG, "mgx_prolong_add: bad level");
     if (c->dist) return no_dist(c, "mgx_prolong_add");
+    drop_spec(c);
     return op_prolong_add(c, level);
 }
 int mgx_vcycle(mgx_ctx *c) {
@@ -798,6 +895,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgx::set_march_block(value);
         return MGX_OK;
     }
+    if (!strcmp(key, "cross_cycle")) {
+        if (value != 0 && value != 1) return fail(MGX_E_ARG, "cross_cycle must be 0 or 1");
+        mgxi::g_cross_cycle = value;
+        return MGX_OK;
+    }
     if (!strcmp(key, "march_kernel")) {
         if (value < 0 || value > 2) return fail(MGX_E_ARG, "march_kernel must be 0, 1 or 2");
         mgx::set_march_kernel(value);
@@ -818,6 +920,11 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "march_block")) {
         *value = mgx::get_march_block();
+        return MGX_OK;
+    }
+    if (!strcmp(key, "cross_cycle")) {
+        mgxi::cross_cycle_on();
+        *value = mgxi::g_cross_cycle;
         return MGX_OK;
     }
     if (!strcmp(key, "march_kernel")) {

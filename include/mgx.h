@@ -157,6 +157,11 @@ int mgx_synchronize(mgx_ctx *ctx);
  * fused smoothing pass as 2-D LDS tiles instead of the row march (default 2048;
  * env MGX_TILE_MAX_N).  "march_block": lanes per workgroup of the row march on
  * levels with n >= 4096, 128 or 256 (default 256; env MGX_MARCH_BLOCK).
+ * "cross_cycle": 1 (default) fuses, inside mg_outer / run_cycles / step, the
+ * finest level's post-smoothing of each V-cycle with the pre-smoothing of
+ * the next into one HBM pass (levels with n >= 4096, V-cycles, nsmooth 2 or
+ * 3; bitwise the same results); after such a cycle the coarse levels hold
+ * the next cycle's restricted rhs, not the last correction.  0 = off.
  * "march_kernel": row march on levels with n >= 4096: 1 wave-private
  * registers + DPP (default), 0 workgroup with an LDS ring (env MGX_MARCH_KERNEL).
  * "dist_min_rows": partitioned solvers replicate every level whose row blocks
@@ -173,7 +178,8 @@ int mgx_get_tuning(const char *key, long *value);
 #define MGX_K_RHS 5            /* compute_rhs */
 #define MGX_K_HALO 6           /* halo exchange (multi-GPU) */
 #define MGX_K_PSMOOTH 7        /* prolongation + add fused into a smoothing pass */
-#define MGX_K_COUNT 8
+#define MGX_K_XSMOOTH 8        /* finest level: post-smoothing of cycle k + pre-smoothing of k+1 */
+#define MGX_K_COUNT 9
 /* on: 0 off, 1 every launch, 2 finest-level launches only (two events per
  * recorded launch; mode 2 keeps the overhead off the small levels). */
 int mgx_profile_enable(mgx_ctx *ctx, int on);
