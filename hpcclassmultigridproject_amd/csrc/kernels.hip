@@ -795,22 +795,26 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
             }
         };
         // u row R (+ prolongation) as it enters the ring
-        auto make_u = [&](int R, const UPre &u) {
+        // (row parity `odd` is a compile-time constant at every call site; the
+        // range test is a select: branches here make the waitcnt pass drain
+        // the prefetch queue)
+        auto make_u = [&](int R, const UPre &u, const bool odd) {
             double2 v = u.X;
             if (C::ZERO) v = make_double2(0.0, 0.0);
-            if (C::PROL && act && R >= 0 && R <= n) {
+            if (C::PROL) {
                 double2 pr;
                 const double q01 = j1 ? u.q01 : 0.0;
                 const double q11 = j1 ? u.q11 : 0.0;
-                if (!(R & 1)) {
+                if (!odd) {
                     pr.x = u.q00;
                     pr.y = (u.q00 + q01) / 2;
                 } else {
                     pr.x = (u.q00 + u.q10) / 2;
                     pr.y = (u.q00 + u.q10 + q01 + q11) / 4;
                 }
-                v.x = v.x + pr.x;
-                v.y = v.y + pr.y;
+                const bool on = act && R >= 0 && R <= n;
+                v.x = on ? v.x + pr.x : v.x;
+                v.y = on ? v.y + pr.y : v.y;
             }
             return v;
         };
@@ -840,7 +844,7 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
             load_u(s + d, up[0]);
-            ur[d] = make_u(s + d, up[0]);
+            ur[d] = make_u(s + d, up[0], d & 1);
         }
         load_u(s + 3, up[1]);
         load_u(s + 4, up[0]);
@@ -851,7 +855,7 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
 #pragma unroll
             for (int p = 0; p < NR; ++p) {
                 // (1) u row s+3 enters the ring; its prefetch set takes row s+5
-                ur[(p + 3) % NR] = make_u(s + 3, up[(p + 1) & 1]);
+                ur[(p + 3) % NR] = make_u(s + 3, up[(p + 1) & 1], (p + 3) & 1);
                 load_u(s + 5, up[(p + 1) & 1]);
                 // (2) the S smoothing stages
 #pragma unroll
@@ -1014,22 +1018,22 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             u.q10 = p1[0];
             u.q11 = p1[j1];
         };
-        auto make_u = [&](int R, const UPre &u) {   // + prolongation (gs.cpp:238-265)
+        // + prolongation (gs.cpp:238-265); static parity, select (see k_wsmooth)
+        auto make_u = [&](int R, const UPre &u, const bool odd) {
             double2 v = u.X;
-            if (act && R >= 0 && R <= n) {
-                double2 pv;
-                const double q01 = j1 ? u.q01 : 0.0;
-                const double q11 = j1 ? u.q11 : 0.0;
-                if (!(R & 1)) {
-                    pv.x = u.q00;
-                    pv.y = (u.q00 + q01) / 2;
-                } else {
-                    pv.x = (u.q00 + u.q10) / 2;
-                    pv.y = (u.q00 + u.q10 + q01 + q11) / 4;
-                }
-                v.x = v.x + pv.x;
-                v.y = v.y + pv.y;
+            double2 pv;
+            const double q01 = j1 ? u.q01 : 0.0;
+            const double q11 = j1 ? u.q11 : 0.0;
+            if (!odd) {
+                pv.x = u.q00;
+                pv.y = (u.q00 + q01) / 2;
+            } else {
+                pv.x = (u.q00 + u.q10) / 2;
+                pv.y = (u.q00 + u.q10 + q01 + q11) / 4;
             }
+            const bool on = act && R >= 0 && R <= n;
+            v.x = on ? v.x + pv.x : v.x;
+            v.y = on ? v.y + pv.y : v.y;
             return v;
         };
         auto load_rv = [&](int R, RowData &d) {
@@ -1054,25 +1058,24 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             ur[q] = make_double2(0.0, 0.0);
             rd[q].r = rd[q].x = rd[q].y = make_double2(0.0, 0.0);
         }
+        // one loop per role (a role branch inside the step would make the
+        // waitcnt pass see A's pending loads on B's path and drain them)
+        int it = 0;
         if (isA) {
 #pragma unroll
             for (int d = 0; d < 3; ++d) {
                 load_u(s0 + d, up[0]);
-                ur[d] = make_u(s0 + d, up[0]);
+                ur[d] = make_u(s0 + d, up[0], d & 1);
             }
             load_u(s0 + 3, up[1]);
             load_u(s0 + 4, up[0]);
             load_rv(s0 + 1, rd[1]);
             load_rv(s0 + 2, rd[2]);
-        }
-
-        int it = 0;
-        for (;;) {
+            for (;;) {
 #pragma unroll
-            for (int p = 0; p < NR; ++p) {
-                if (isA) {
+                for (int p = 0; p < NR; ++p) {
                     const int s = s0 + it;
-                    ur[(p + 3) % NR] = make_u(s + 3, up[(p + 1) & 1]);
+                    ur[(p + 3) % NR] = make_u(s + 3, up[(p + 1) & 1], (p + 3) & 1);
                     load_u(s + 5, up[(p + 1) & 1]);
 #pragma unroll
                     for (int h = 0; h < S; ++h) {
@@ -1110,7 +1113,15 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         if (keep && ro >= a && ro < b) st2((upost + (long)ro * pitch) + c0, uf);
                     }
                     load_rv(s + 3, rd[(p + 3) % NR]);
-                } else {
+                    __syncthreads();
+                    if (++it == iters) goto done_a;
+                }
+            }
+        done_a:;
+        } else {
+            for (;;) {
+#pragma unroll
+                for (int p = 0; p < NR; ++p) {
                     const int s = s0 + it - D;   // B's ring phase q = p - D (mod NR)
                     constexpr int dq = ((D % NR) + NR) % NR;
                     const int q = (p - dq + NR) % NR;   // compile-time after unrolling
@@ -1186,12 +1197,12 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                             (rhsc + (long)(r >> 1) * pitchc)[c0 >> 1] = res;
                         }
                     }
+                    __syncthreads();
+                    if (++it == iters) goto done_b;
                 }
-                __syncthreads();
-                if (++it == iters) goto done;
             }
+        done_b:;
         }
-    done:;
     }
     if (!isA) {
         const double tot = wave_sum(acc);
