@@ -102,7 +102,8 @@ int launch(mgx_ctx *c, int kind, int level, double bytes, F &&f) {
 int prof_flush(mgx_ctx *c);
 int materialize(mgx_ctx *c, int l);
 int read_norm(mgx_ctx *c, double *norm);
-int op_vcycle(mgx_ctx *c, int l, double *norm = nullptr);
+// store_post: see op_cross (false only between cycles of one run_cycles call)
+int op_vcycle(mgx_ctx *c, int l, double *norm = nullptr, bool store_post = true);
 int op_rhs(mgx_ctx *c);
 int op_residual_norm(mgx_ctx *c, int l, double *norm, double bytes_per_pt = 48.0);
 int build_tower(mgx_ctx *c);

@@ -93,6 +93,7 @@ struct XArgs {
     double *partials = nullptr, *norm_out = nullptr;
     long n = 0, pitch = 0;
     Coef c{};
+    bool store_post = true;   // false: u_post only feeds the norm (not the last cycle)
 };
 int launch_xsmooth(const XArgs &a, int sweeps, hipStream_t s);
 // Levels with n <= tile_max_n use the 2-D tile form of the fused pass (small

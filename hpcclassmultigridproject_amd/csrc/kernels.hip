@@ -966,7 +966,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     const double *__restrict__ rhs, const double *__restrict__ v1, const double *__restrict__ v2,
     const double *__restrict__ uc, long pitchc, double *__restrict__ rhsc,
     double *__restrict__ partials, int n, long pitch, int groups, long units_per_wg, Coef c,
-    int lo, int hi) {
+    int lo, int hi, int store_post) {
     using X = XCfg<K>;
     constexpr int S = X::S, H = X::H, NR = X::NR, W = X::W, D = X::D, NU = X::NU,
                   NRD = X::NRD, EA = X::EA, EB = X::EB;
@@ -1110,7 +1110,8 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         const int ro = s + 2 - S;
                         const double2 uf = ur[(p + 2 - S + 2 * NR) % NR];
                         uring[pr][ro & (NU - 1)][l] = uf;
-                        if (keep && ro >= a && ro < b) st2((upost + (long)ro * pitch) + c0, uf);
+                        if (store_post && keep && ro >= a && ro < b)
+                            st2((upost + (long)ro * pitch) + c0, uf);
                     }
                     load_rv(s + 3, rd[(p + 3) % NR]);
                     __syncthreads();
@@ -1709,7 +1710,7 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
 #endif
     MGX_LAUNCH((k_xsmooth<WPB, K>), dim3(grid), dim3(128 * WPB), s, A.uin, A.upost, A.upre,
                A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, A.partials, (int)n, A.pitch, groups,
-               upw, A.c, lo, hi);
+               upw, A.c, lo, hi, A.store_post ? 1 : 0);
     return (int)grid * WPB;
 }
 

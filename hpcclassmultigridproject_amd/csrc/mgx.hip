@@ -262,7 +262,7 @@ void drop_spec(mgx_ctx *c) {
 // here) into one free buffer, u_pre (cycle k+1's pre-smoothing) into the
 // other, the residual of u_post -> c->dscal[0], the restriction of u_pre's
 // residual -> rhs[1] (u[1] flagged zero for cycle k+1).
-static int op_cross(mgx_ctx *c) {
+static int op_cross(mgx_ctx *c, bool store_post) {
     Level &L = c->lv[0], &Cl = c->lv[1];
     CHK(materialize(c, 1));
     int P = -1, Q = -1;
@@ -283,6 +283,7 @@ static int op_cross(mgx_ctx *c) {
     A.n = L.n;
     A.pitch = L.pitch;
     A.c = L.coef;
+    A.store_post = store_post;
     const int k = c->opt.nsmooth;
     // algorithmic bytes: prolong+add, k sweeps, residual+norm (post of cycle
     // k) + k sweeps, residual+restriction (pre of cycle k+1), SURVEY 8d
@@ -307,7 +308,7 @@ static int op_cross(mgx_ctx *c) {
 // cycle and the pre-smoothing of the NEXT one are one k_xsmooth pass, so a
 // cycle is [pre (first cycle only) | coarse levels | cross pass]; a cycle that
 // follows one starts from the speculative state the cross pass left.
-int op_vcycle(mgx_ctx *c, int l, double *norm) {
+int op_vcycle(mgx_ctx *c, int l, double *norm, bool store_post) {
     if (l == 0 && norm && cross_ok(c)) {
         Level &L = c->lv[0];
         if (L.spec >= 0) {   // pre-smoothing + restriction already done
@@ -317,7 +318,7 @@ int op_vcycle(mgx_ctx *c, int l, double *norm) {
             CHK(op_smooth(c, 0, c->opt.nsmooth, false, /*restrict=*/true, false, nullptr));
         }
         CHK(op_vcycle(c, 1));
-        CHK(op_cross(c));
+        CHK(op_cross(c, store_post));
         return read_norm(c, norm);
     }
     if (l == 0) drop_spec(c);
@@ -353,9 +354,11 @@ int op_rhs(mgx_ctx *c) {
 
 // mg_outer (multigrid.cpp:97-120).
 // one V-cycle + the residual norm after it, single GPU or partitioned
-int cycle_norm(mgx_ctx *c, double *res) {
+// store_post = false: the caller runs another cycle right away, so this
+// cycle's solution is never observed (only its norm); skip writing it
+int cycle_norm(mgx_ctx *c, double *res, bool store_post = true) {
     if (c->dist) return dist_vcycle(c, res);
-    return op_vcycle(c, 0, res);
+    return op_vcycle(c, 0, res, store_post);
 }
 int norm0(mgx_ctx *c, double *res) {
     if (c->dist) return dist_residual_norm(c, res);
@@ -728,7 +731,7 @@ int mgx_step(mgx_ctx *c, double tol, int *cycles) {
 int mgx_run_cycles(mgx_ctx *c, int cycles, double *res) {
     if (!c || cycles < 0) return fail(MGX_E_ARG, "mgx_run_cycles: bad args");
     double r = 0;
-    for (int k = 0; k < cycles; ++k) CHK(cycle_norm(c, &r));
+    for (int k = 0; k < cycles; ++k) CHK(cycle_norm(c, &r, /*store_post=*/k == cycles - 1));
     if (res) *res = r;
     return MGX_OK;
 }

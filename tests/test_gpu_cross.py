@@ -69,3 +69,26 @@ def test_cross_cycle_mg_outer_and_steps(cross):
     assert np.array_equal(u0_, u1_) and np.array_equal(uf0, uf1)
     for a, b in ((r00, r01), (s00, s01), (s0, s1)):
         assert abs(a - b) <= NORM_RTOL * abs(a)
+
+
+def test_run_cycles_batch_equals_single_calls(cross):
+    """run_cycles(K) skips writing the intermediate cycles' solutions (only
+    their norms are observed); the final state and norm must be identical."""
+    cross(1)
+    N, L = 4096, 6
+    u0, v1, v2 = init_problem(N)
+    out = []
+    for batch in (False, True):
+        with Multigrid(N, L, 1.0 / N / 10, NU) as mg:
+            mg.upload(u0, v1, v2)
+            mg.rhs()
+            if batch:
+                r = mg.run_cycles(4)
+            else:
+                for _ in range(4):
+                    r = mg.run_cycles(1)
+            r_after = mg.residual_norm(0)
+            out.append((mg.download(), r, r_after))
+    (ua, ra, raa), (ub, rb, rab) = out
+    assert np.array_equal(ua, ub)
+    assert ra == rb and raa == rab
