@@ -119,7 +119,7 @@ int dist_upload(mgx_ctx *c, const double *u0, const double *v1, const double *v2
                 hipMemcpyKind kind);
 int dist_download(mgx_ctx *c, double *u, hipMemcpyKind kind);
 int dist_rhs(mgx_ctx *c);
-int dist_vcycle(mgx_ctx *c, double *norm);
+int dist_vcycle(mgx_ctx *c, double *norm, bool store_post = true);
 int dist_residual_norm(mgx_ctx *c, double *norm);
 void dist_free(mgx_ctx *c);
 // replicated coarse-level contexts of a partitioned context (one per local part)
@@ -129,5 +129,8 @@ int dist_la(mgx_ctx *c);
 // levels whose row blocks would be shorter than this are replicated (tuning
 // key "dist_min_rows", default 256)
 extern long g_dist_min_rows;
+// tuning key "cross_cycle" (mgx.hip); levels with n >= kCrossMinN can use it
+bool cross_cycle_on();
+constexpr long kCrossMinN = 4096;
 
 }  // namespace mgxi

@@ -33,7 +33,8 @@
 
 namespace mgxi {
 
-constexpr int kGhost = 8;            // >= the widest fused-pass cone (E <= 7) + 1
+constexpr int kGhost = 8;        // >= the widest fused-pass cone (E <= 7) + 1
+constexpr int kGhostFine = 16;   // level 0: the cross-cycle pass's cone is 14 rows
 long g_dist_min_rows = 256;
 
 #define NCCLCHK(expr)                                                                    \
@@ -47,11 +48,13 @@ struct PLevel {
     long n = 0, pitch = 0;
     int ra = 0, rb = 0;   // owned rows [ra, rb)
     int lo = 0, hi = 0;   // allocated rows [lo, hi] (owned + ghosts, clipped to [0, n])
-    double *u[2] = {nullptr, nullptr};
+    double *u[3] = {nullptr, nullptr, nullptr};   // u[2]: level 0, cross-cycle pass
     int cur = 0;
+    int spec = -1;   // level 0: buffer of the next cycle's pre-smoothed u (Level::spec)
     bool zero = false;
     double *rhs = nullptr, *v1 = nullptr, *v2 = nullptr;
     mgx::Coef coef{};
+    int nxt() const { return cur == 0 ? 1 : 0; }
     // field pointer offset so that F(a) + r*pitch is global row r
     double *F(double *a) const { return a - (long)lo * pitch; }
     double *U() const { return F(u[cur]); }
@@ -97,6 +100,7 @@ void dist_free(mgx_ctx *c) {
         for (auto &L : p.lv) {
             (void)hipFree(L.u[0]);
             (void)hipFree(L.u[1]);
+            (void)hipFree(L.u[2]);
             (void)hipFree(L.rhs);
             (void)hipFree(L.v1);
             (void)hipFree(L.v2);
@@ -125,10 +129,13 @@ static int build_dist(mgx_ctx *c, int world, const std::vector<int> &ranks) {
             L.pitch = mgx::tower_pitch(L.n);
             L.coef = mgx::make_coef(c->dt, c->nu, h);
             plan_rows(c->N, l, world, r, &L.ra, &L.rb);
-            L.lo = std::max(0, L.ra - kGhost);
-            L.hi = (int)std::min<long>(L.n, (long)L.rb - 1 + kGhost);
-            double **bufs[5] = {&L.u[0], &L.u[1], &L.rhs, &L.v1, &L.v2};
+            const int g = l == 0 ? kGhostFine : kGhost;
+            L.lo = std::max(0, L.ra - g);
+            L.hi = (int)std::min<long>(L.n, (long)L.rb - 1 + g);
+            const bool third = l == 0 && L.n >= kCrossMinN;
+            double **bufs[6] = {&L.u[0], &L.u[1], &L.rhs, &L.v1, &L.v2, &L.u[2]};
             for (double **b : bufs) {
+                if (b == &L.u[2] && !third) continue;
                 HIPCHK(hipMalloc(b, L.bytes()));
                 HIPCHK(hipMemsetAsync(*b, 0, L.bytes(), c->stream));
             }
@@ -257,7 +264,7 @@ static int reduce_norm(mgx_ctx *c, double *norm) {
 static mgx::SmoothArgs args_for(const PLevel &L) {
     mgx::SmoothArgs A{};
     A.uin = L.U();
-    A.uout = L.F(L.u[L.cur ^ 1]);
+    A.uout = L.F(L.u[L.nxt()]);
     A.rhs = L.F(L.rhs);
     A.v1 = L.F(L.v1);
     A.v2 = L.F(L.v2);
@@ -315,7 +322,7 @@ static int smooth(mgx_ctx *c, int l, bool prolong, bool restrict_, bool norm) {
             CHK(launch(c, pr ? MGX_K_PSMOOTH : MGX_K_GS, l, bytes,
                        [&] { blocks = mgx::launch_smooth(A, k, mode, c->stream); }));
             if (blocks < 0) return fail(MGX_E_ARG, "launch_smooth: unsupported sweeps/mode");
-            L.cur ^= 1;
+            L.cur = L.nxt();
             L.zero = false;
         }
         done += k;
@@ -323,30 +330,130 @@ static int smooth(mgx_ctx *c, int l, bool prolong, bool restrict_, bool norm) {
     return MGX_OK;
 }
 
-static int dist_level(mgx_ctx *c, int l, bool want_norm) {
+// rhs of level l+1 restricted (owned rows): refresh its ghosts, or gather it
+// into the replicated sub-contexts; u[l+1] = 0 for the coming coarse solve
+static int coarse_rhs_ready(mgx_ctx *c, int l) {
     Dist *d = c->dist;
+    if (l + 1 < d->la) {
+        CHK(exchange(c, l + 1, kRhs));
+        for (auto &p : d->parts) p.lv[l + 1].zero = true;
+        return MGX_OK;
+    }
+    return gather_rhs(c);
+}
+
+static int coarse_cycle(mgx_ctx *c, int l);
+
+static int dist_level(mgx_ctx *c, int l, bool want_norm) {
     for (int sh = 0; sh < c->opt.shape; ++sh) {
         const bool last = sh == c->opt.shape - 1;
         CHK(smooth(c, l, false, /*restrict=*/true, false));
-        if (l + 1 < d->la) {
-            CHK(exchange(c, l + 1, kRhs));
-            for (auto &p : d->parts) p.lv[l + 1].zero = true;
-            CHK(dist_level(c, l + 1, false));
-        } else {
-            CHK(gather_rhs(c));
-            for (auto &p : d->parts) CHK(op_vcycle(p.sub, 0));
-        }
+        CHK(coarse_rhs_ready(c, l));
+        CHK(coarse_cycle(c, l + 1));
         CHK(smooth(c, l, /*prolong=*/true, false, want_norm && last));
     }
     return MGX_OK;
 }
 
-int dist_vcycle(mgx_ctx *c, double *norm) {
+// the V-cycle below a partitioned level l-1: partitioned or replicated
+static int coarse_cycle(mgx_ctx *c, int l) {
+    Dist *d = c->dist;
+    if (l < d->la) return dist_level(c, l, false);
+    for (auto &p : d->parts) CHK(op_vcycle(p.sub, 0));
+    return MGX_OK;
+}
+
+static bool dist_cross_ok(mgx_ctx *c) {
+    Dist *d = c->dist;
+    return cross_cycle_on() && d->la >= 1 && d->parts[0].lv[0].u[2] &&
+           c->opt.smoother == 0 && c->opt.shape == 1 &&
+           (c->opt.nsmooth == 2 || c->opt.nsmooth == 3) && c->opt.fuse >= c->opt.nsmooth;
+}
+
+static void dist_drop_spec(mgx_ctx *c) {
+    for (auto &p : c->dist->parts)
+        if (!p.lv.empty()) p.lv[0].spec = -1;
+}
+
+// Cross-cycle pass on the row blocks of level 0 (mgx.hip:op_cross): u ghosts
+// (16 rows: the pass's cone is 14) and, if level 1 is partitioned, its u
+// ghosts for the prolongation; afterwards the restricted rhs of the next cycle
+// is made ready on level 1 and the per-rank norm sums are reduced by the caller.
+static int dist_cross(mgx_ctx *c, bool store_post) {
+    Dist *d = c->dist;
+    CHK(exchange(c, 0, kU));
+    if (1 < d->la) CHK(exchange(c, 1, kU));
+    for (auto &p : d->parts) {
+        PLevel &L = p.lv[0];
+        int P = -1, Q = -1;
+        for (int i = 0; i < 3; ++i)
+            if (i != L.cur) (P < 0 ? P : Q) = i;
+        mgx::XArgs A;
+        A.uin = L.U();
+        A.upost = L.F(L.u[P]);
+        A.upre = L.F(L.u[Q]);
+        A.rhs = L.F(L.rhs);
+        A.v1 = L.F(L.v1);
+        A.v2 = L.F(L.v2);
+        double Mc;
+        if (1 < d->la) {
+            PLevel &Cl = p.lv[1];
+            A.uc = Cl.U();
+            A.rhsc = Cl.F(Cl.rhs);
+            A.pitchc = Cl.pitch;
+            Mc = Cl.Mown();
+        } else {
+            Level &Cl = p.sub->lv[0];
+            A.uc = Cl.U();
+            A.rhsc = Cl.rhs;
+            A.pitchc = Cl.pitch;
+            Mc = L.Mown() / 4;
+        }
+        A.partials = c->partials;
+        A.norm_out = p.dsum;
+        A.norm_sqrt = false;
+        A.n = L.n;
+        A.pitch = L.pitch;
+        A.c = L.coef;
+        A.store_post = store_post;
+        A.ra = L.ra;
+        A.rb = L.rb;
+        A.lo = L.lo;
+        A.hi = L.hi;
+        const int k = c->opt.nsmooth;
+        const double bytes = (32.0 + 40.0 * k + 48.0 + 40.0 * k + 40.0) * L.Mown() + 32.0 * Mc;
+        int blocks = 0;
+        CHK(launch(c, MGX_K_XSMOOTH, 0, bytes,
+                   [&] { blocks = mgx::launch_xsmooth(A, k, c->stream); }));
+        if (blocks < 0) return fail(MGX_E_ARG, "launch_xsmooth: unsupported sweeps / block");
+        L.cur = P;
+        L.spec = Q;
+        L.zero = false;
+    }
+    return coarse_rhs_ready(c, 0);
+}
+
+int dist_vcycle(mgx_ctx *c, double *norm, bool store_post) {
     Dist *d = c->dist;
     if (d->la == 0) {   // everything replicated
-        for (auto &p : d->parts) CHK(op_vcycle(p.sub, 0, norm));
+        for (auto &p : d->parts) CHK(op_vcycle(p.sub, 0, norm, store_post));
         return MGX_OK;
     }
+    if (norm && dist_cross_ok(c)) {
+        if (d->parts[0].lv[0].spec >= 0) {   // pre-smoothing + restriction done
+            for (auto &p : d->parts) {
+                p.lv[0].cur = p.lv[0].spec;
+                p.lv[0].spec = -1;
+            }
+        } else {
+            CHK(smooth(c, 0, false, /*restrict=*/true, false));
+            CHK(coarse_rhs_ready(c, 0));
+        }
+        CHK(coarse_cycle(c, 1));
+        CHK(dist_cross(c, store_post));
+        return reduce_norm(c, norm);
+    }
+    dist_drop_spec(c);
     CHK(dist_level(c, 0, norm != nullptr));
     if (norm) CHK(reduce_norm(c, norm));
     return MGX_OK;
@@ -372,6 +479,7 @@ int dist_residual_norm(mgx_ctx *c, double *norm) {
 
 int dist_rhs(mgx_ctx *c) {
     Dist *d = c->dist;
+    dist_drop_spec(c);
     if (d->la == 0) {
         for (auto &p : d->parts) CHK(op_rhs(p.sub));
         return MGX_OK;
@@ -417,6 +525,7 @@ int dist_upload(mgx_ctx *c, const double *u0, const double *v1, const double *v2
                      (l > 0 ? hipMemsetAsync(L.u[0], 0, cnt, c->stream) : hipSuccess);
             if (rc) rc = fail(MGX_E_HIP, "dist_upload: copy");
             L.cur = 0;
+            L.spec = -1;
             L.zero = false;
         }
         for (int l = d->la; rc == MGX_OK && l < c->L; ++l) {

@@ -82,7 +82,8 @@ int launch_smooth(const SmoothArgs &a, int sweeps, int mode, hipStream_t s);
 // (u_in + P(uc), `sweeps` sweeps, residual norm -> *norm_out as sqrt) into
 // upost, and the pre-smoothing of cycle k+1 (`sweeps` sweeps, residual
 // restricted into rhsc) into upre.  sweeps 2 or 3; returns the partials count
-// or -1.  Whole level only (no row partition).
+// or -1.  A row block [ra, rb) needs its rows [ra-14, rb+14) valid in the
+// inputs (the pass's cone) and the matching coarse rows.
 struct XArgs {
     const double *uin = nullptr;
     double *upost = nullptr, *upre = nullptr;
@@ -94,6 +95,8 @@ struct XArgs {
     long n = 0, pitch = 0;
     Coef c{};
     bool store_post = true;   // false: u_post only feeds the norm (not the last cycle)
+    bool norm_sqrt = true;    // false: *norm_out = sum of squares (multi-GPU partial)
+    int ra = 0, rb = -1, lo = 0, hi = -1;   // row block (rb < 0: whole level), as SmoothArgs
 };
 int launch_xsmooth(const XArgs &a, int sweeps, hipStream_t s);
 // Levels with n <= tile_max_n use the 2-D tile form of the fused pass (small

@@ -966,7 +966,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     const double *__restrict__ rhs, const double *__restrict__ v1, const double *__restrict__ v2,
     const double *__restrict__ uc, long pitchc, double *__restrict__ rhsc,
     double *__restrict__ partials, int n, long pitch, int groups, long units_per_wg, Coef c,
-    int lo, int hi, int store_post) {
+    int ra, int rb, int lo, int hi, int store_post) {
     using X = XCfg<K>;
     constexpr int S = X::S, H = X::H, NR = X::NR, W = X::W, D = X::D, NU = X::NU,
                   NRD = X::NRD, EA = X::EA, EB = X::EB;
@@ -978,7 +978,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     const int wv = threadIdx.x >> 6;
     const bool isA = wv < WPB;   // wave-uniform role
     const int pr = isA ? wv : wv - WPB;
-    const int nrows = n + 1;
+    const int nrows = rb - ra;   // owned rows [ra, rb) (a row block on multi-GPU)
     const long total = (long)groups * nrows;
     long start = (long)blockIdx.x * units_per_wg;
     const long end = min(total, start + units_per_wg);
@@ -988,8 +988,8 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
 
     while (start < end) {
         const int grp = (int)(start / nrows);
-        const int a = (int)(start % nrows);
-        const int b = (int)min((long)nrows, (long)a + (end - start));
+        const int a = ra + (int)(start % nrows);
+        const int b = (int)min((long)rb, (long)a + (end - start));
         start += b - a;
 
         const int j0 = (grp * WPB + pr) * W;
@@ -1698,23 +1698,30 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
         slots = std::max(1, cus) * std::max(1, per);
     }
     const long n = A.n;
+    int ra = A.ra, rb = A.rb, lo = A.lo, hi = A.hi;
+    if (rb < 0) {
+        ra = 0;
+        rb = (int)n + 1;
+        lo = 0;
+        hi = (int)n;
+    }
     const int groups = (int)((n + 1 + (long)W * WPB - 1) / ((long)W * WPB));
-    const long total = (long)groups * (n + 1);
+    const long total = (long)groups * (rb - ra);
     long g = std::max<long>(1, std::min<long>(slots, total / 64));
     g = std::min<long>(g, kNormBlocks / WPB);
     const long upw = (total + g - 1) / g;
     const unsigned grid = (unsigned)((total + upw - 1) / upw);
-    int lo = 0, hi = (int)n;
 #ifdef MGX_PROBE_CLAMP
     lo = hi = 2;   // experiment build only: every load from one row (L2-resident)
 #endif
     MGX_LAUNCH((k_xsmooth<WPB, K>), dim3(grid), dim3(128 * WPB), s, A.uin, A.upost, A.upre,
                A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, A.partials, (int)n, A.pitch, groups,
-               upw, A.c, lo, hi, A.store_post ? 1 : 0);
+               upw, A.c, ra, rb, lo, hi, A.store_post ? 1 : 0);
     return (int)grid * WPB;
 }
 
 int launch_xsmooth(const XArgs &A, int sweeps, hipStream_t s) {
+    if (A.rb >= 0 && (A.ra & 1)) return -1;   // row blocks start at even rows
     int blocks = -1;
     // 4 strip pairs per workgroup (one workgroup of 8 waves per CU): adjacent
     // 1-KiB row pieces of four strips per load (measured: 4.05 ms vs 4.13 ms
@@ -1726,7 +1733,7 @@ int launch_xsmooth(const XArgs &A, int sweeps, hipStream_t s) {
     }
     if (blocks > 0)
         MGX_LAUNCH(k_norm_final, dim3(1), dim3(kFinalThreads), s, (const double *)A.partials,
-                   blocks, A.norm_out, 1);
+                   blocks, A.norm_out, A.norm_sqrt ? 1 : 0);
     return blocks;
 }
 
@@ -1786,7 +1793,25 @@ long get_march_block() { return march_block(); }
 
 template <int K, int MODE>
 static int smooth_block(const SmoothArgs &A, hipStream_t s) {
-    if (A.n <= tile_max_n()) {
+    // the row march needs >= ~32 rows per wave to amortise its priming rows;
+    // a row block too small to give every resident wave that much (a
+    // partitioned level on many GPUs) runs as LDS tiles instead
+    bool tile = A.n <= tile_max_n();
+    if (!tile && march_kernel() == 1) {
+        constexpr int W4 = WCfg<K, MODE>::W * 4;
+        static int slots = 0;
+        if (!slots) {
+            int dev = 0, cus = 0, per = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_wsmooth<4, K, MODE>, 256,
+                                                               0);
+            slots = std::max(1, cus) * std::max(1, per);
+        }
+        const long groups = (A.n + 1 + W4 - 1) / W4;
+        tile = groups * (A.rb - A.ra) < (long)slots * 32;
+    }
+    if (tile) {
         const int g = smooth_tile_inst<K, MODE>(A, s);
         if (g > 0) return g;
     }

@@ -24,9 +24,8 @@ thread_local std::string g_err;
 
 // Cross-cycle fusion of the finest level (k_xsmooth) on levels this large
 // (the row-march regime); tuning key "cross_cycle" turns it off.
-constexpr long kCrossMinN = 4096;
 long g_cross_cycle = -1;
-static bool cross_cycle_on() {
+bool cross_cycle_on() {
     if (g_cross_cycle < 0) {
         const char *e = getenv("MGX_CROSS_CYCLE");
         g_cross_cycle = e ? atol(e) : 1;
@@ -357,7 +356,7 @@ int op_rhs(mgx_ctx *c) {
 // store_post = false: the caller runs another cycle right away, so this
 // cycle's solution is never observed (only its norm); skip writing it
 int cycle_norm(mgx_ctx *c, double *res, bool store_post = true) {
-    if (c->dist) return dist_vcycle(c, res);
+    if (c->dist) return dist_vcycle(c, res, store_post);
     return op_vcycle(c, 0, res, store_post);
 }
 int norm0(mgx_ctx *c, double *res) {

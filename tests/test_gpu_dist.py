@@ -192,3 +192,31 @@ def test_partitioned_create_errors():
         Multigrid(256, 4, 1e-3, NU, local_parts=2, smoother=1)
     with pytest.raises(MGXError):
         Multigrid(256, 4, 1e-3, NU, local_parts=2, nsmooth=0)
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_cross_cycle_partitioned_equals_single_N4096(G):
+    """Finest level >= 4096: the cross-cycle pass runs on the row blocks
+    (16 ghost rows), in single-cycle calls, batched run_cycles and mg_outer."""
+    N, L = 4096, 6
+    dt = 1.0 / N / 10
+    u0, v1, v2 = init_problem(N)
+    out = []
+    for parts in (0, G):
+        with Multigrid(N, L, dt, NU, local_parts=parts) as mg:
+            mg.upload(u0, v1, v2)
+            mg.rhs()
+            mg.profile(True)
+            n1 = [mg.run_cycles(1) for _ in range(2)]
+            n3 = mg.run_cycles(3)
+            xs = mg.profile_get(_lib.K_XSMOOTH)[0]
+            mg.profile(False)
+            u_a = mg.download()
+            cyc, r0, r, _ = mg.mg_outer(1e-10)
+            out.append((n1, n3, xs, u_a, cyc, r0, r, mg.download()))
+    s, p = out
+    assert s[2] == 5 and p[2] == 5 * G   # one cross pass per cycle (per part)
+    assert np.array_equal(p[3], s[3]) and np.array_equal(p[7], s[7])
+    assert p[4] == s[4]
+    np.testing.assert_allclose(p[0] + [p[1], p[5], p[6]], s[0] + [s[1], s[5], s[6]],
+                               rtol=NORM_RTOL)
