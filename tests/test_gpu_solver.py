@@ -154,3 +154,42 @@ def test_run_cycles_is_deterministic():
             r = mg.run_cycles(3)
             outs.append((mg.download(), r))
     assert np.array_equal(outs[0][0], outs[1][0]) and outs[0][1] == outs[1][1]
+
+
+@pytest.mark.parametrize("N", [64, 128])
+def test_coarsest_solve_to_rounding_matches_direct_solve(N):
+    """SURVEY 8f item 4 (the intent of exact_solve.cpp): the coarsest-level
+    solve driven to rounding (coarse_tol -> 1e-13) equals a sparse direct
+    solve of the same Crank-Nicolson operator (gs.cpp:126-130 coefficients,
+    level velocities, Dirichlet 0) to 1e-12 relative."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spla
+    u0, v1, v2 = init_problem(N)
+    dt, h = 1.0 / N / 10, 1.0 / N
+    with Multigrid(N, 1, dt, NU, coarse_tol=1e-13, coarse_maxit=1000) as mg:
+        mg.upload(u0, v1, v2)
+        mg.rhs()
+        rhs = mg.download_level(0, "rhs").reshape(N + 1, N + 1)
+        mg.mg_inner()
+        u = mg.download().reshape(N + 1, N + 1)
+        iters = mg.coarse_iterations()
+    V1, V2 = v1.reshape(N + 1, N + 1), v2.reshape(N + 1, N + 1)
+    rr = 0.5 * dt / (h * h)
+    a = lambda v: rr * (-v * h / 2.0 + NU)
+    b = lambda v: rr * (v * h / 2.0 + NU)
+    m = N - 1
+    idx = lambda i, j: (i - 1) * m + (j - 1)
+    rows, cols, vals = [], [], []
+    for i in range(1, N):
+        for j in range(1, N):
+            k = idx(i, j)
+            rows.append(k); cols.append(k); vals.append(1.0 - 4.0 * rr * NU)
+            for (ii, jj, cf) in ((i - 1, j, a(V1[i, j])), (i, j - 1, a(V2[i, j])),
+                                 (i + 1, j, b(V1[i, j])), (i, j + 1, b(V2[i, j]))):
+                if 1 <= ii <= N - 1 and 1 <= jj <= N - 1:
+                    rows.append(k); cols.append(idx(ii, jj)); vals.append(cf)
+    A = sp.csr_matrix((vals, (rows, cols)), shape=(m * m, m * m))
+    x = spla.spsolve(A.tocsc(), rhs[1:N, 1:N].ravel())
+    err = np.max(np.abs(u[1:N, 1:N].ravel() - x)) / np.max(np.abs(x))
+    assert err <= 1e-12, (err, iters)
+    assert iters < 1000
