@@ -435,6 +435,7 @@ static int dist_cross(mgx_ctx *c, bool store_post) {
 
 int dist_vcycle(mgx_ctx *c, double *norm, bool store_post) {
     Dist *d = c->dist;
+    HIPCHK(hipSetDevice(c->device));
     if (d->la == 0) {   // everything replicated
         for (auto &p : d->parts) CHK(op_vcycle(p.sub, 0, norm, store_post));
         return MGX_OK;
@@ -461,6 +462,7 @@ int dist_vcycle(mgx_ctx *c, double *norm, bool store_post) {
 
 int dist_residual_norm(mgx_ctx *c, double *norm) {
     Dist *d = c->dist;
+    HIPCHK(hipSetDevice(c->device));
     if (d->la == 0) {
         for (auto &p : d->parts) CHK(op_residual_norm(p.sub, 0, norm));
         return MGX_OK;
@@ -479,6 +481,7 @@ int dist_residual_norm(mgx_ctx *c, double *norm) {
 
 int dist_rhs(mgx_ctx *c) {
     Dist *d = c->dist;
+    HIPCHK(hipSetDevice(c->device));
     dist_drop_spec(c);
     if (d->la == 0) {
         for (auto &p : d->parts) CHK(op_rhs(p.sub));
@@ -505,6 +508,7 @@ int dist_la(mgx_ctx *c) { return c->dist ? c->dist->la : c->L; }
 int dist_upload(mgx_ctx *c, const double *u0, const double *v1, const double *v2,
                 hipMemcpyKind kind) {
     Dist *d = c->dist;
+    HIPCHK(hipSetDevice(c->device));
     mgx_options o = c->opt;
     o.device = -1;
     mgx_ctx *T = nullptr;
@@ -549,6 +553,7 @@ int dist_upload(mgx_ctx *c, const double *u0, const double *v1, const double *v2
 
 int dist_download(mgx_ctx *c, double *u, hipMemcpyKind kind) {
     Dist *d = c->dist;
+    HIPCHK(hipSetDevice(c->device));
     if (d->la == 0) {
         mgx_ctx *s = d->parts[0].sub;
         Level &L = s->lv[0];
