@@ -24,6 +24,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <initializer_list>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -157,58 +158,78 @@ enum Field { kU, kRhs };
 
 static double *field(const PLevel &L, Field f) { return f == kU ? L.U() : L.F(L.rhs); }
 
-// Refresh the ghost rows of `f` on level l from the neighbouring ranks.
-static int exchange_rows(mgx_ctx *c, int l, Field f) {
+// Refresh the ghost rows of the listed (level, field)s from the neighbouring
+// ranks; over RCCL all of them go in ONE group (one latency, not one each).
+struct XF {
+    int l;
+    Field f;
+};
+
+static int exchange_rows(mgx_ctx *c, std::initializer_list<XF> xs) {
     Dist *d = c->dist;
     if (d->local) {
-        for (size_t i = 0; i < d->parts.size(); ++i) {
-            PLevel &L = d->parts[i].lv[l];
-            const long P = L.pitch;
-            double *dst = field(L, f);
-            if (i > 0) {   // rows [lo, ra) from rank i-1
-                const PLevel &A = d->parts[i - 1].lv[l];
-                HIPCHK(hipMemcpyAsync(dst + (long)L.lo * P, field(A, f) + (long)L.lo * P,
-                                      sizeof(double) * (L.ra - L.lo) * P,
-                                      hipMemcpyDeviceToDevice, c->stream));
+        for (const XF &x : xs)
+            for (size_t i = 0; i < d->parts.size(); ++i) {
+                PLevel &L = d->parts[i].lv[x.l];
+                const long P = L.pitch;
+                double *dst = field(L, x.f);
+                if (i > 0) {   // rows [lo, ra) from rank i-1
+                    const PLevel &A = d->parts[i - 1].lv[x.l];
+                    HIPCHK(hipMemcpyAsync(dst + (long)L.lo * P, field(A, x.f) + (long)L.lo * P,
+                                          sizeof(double) * (L.ra - L.lo) * P,
+                                          hipMemcpyDeviceToDevice, c->stream));
+                }
+                if (i + 1 < d->parts.size()) {   // rows [rb, hi] from rank i+1
+                    const PLevel &B = d->parts[i + 1].lv[x.l];
+                    HIPCHK(hipMemcpyAsync(dst + (long)L.rb * P, field(B, x.f) + (long)L.rb * P,
+                                          sizeof(double) * (L.hi - L.rb + 1) * P,
+                                          hipMemcpyDeviceToDevice, c->stream));
+                }
             }
-            if (i + 1 < d->parts.size()) {   // rows [rb, hi] from rank i+1
-                const PLevel &B = d->parts[i + 1].lv[l];
-                HIPCHK(hipMemcpyAsync(dst + (long)L.rb * P, field(B, f) + (long)L.rb * P,
-                                      sizeof(double) * (L.hi - L.rb + 1) * P,
-                                      hipMemcpyDeviceToDevice, c->stream));
-            }
-        }
         return MGX_OK;
     }
     Part &p = d->parts[0];
-    PLevel &L = p.lv[l];
-    const long P = L.pitch;
-    double *a = field(L, f);
-    NCCLCHK(ncclGroupStart());
-    if (p.rank > 0) {
-        const size_t cnt = (size_t)(L.ra - L.lo) * P;
-        NCCLCHK(ncclSend(a + (long)L.ra * P, cnt, ncclDouble, p.rank - 1, d->comm, c->stream));
-        NCCLCHK(ncclRecv(a + (long)L.lo * P, cnt, ncclDouble, p.rank - 1, d->comm, c->stream));
+    ncclResult_t r = ncclGroupStart();
+    for (const XF &x : xs) {
+        PLevel &L = p.lv[x.l];
+        const long P = L.pitch;
+        double *a = field(L, x.f);
+        if (r == ncclSuccess && p.rank > 0) {
+            const size_t cnt = (size_t)(L.ra - L.lo) * P;
+            r = ncclSend(a + (long)L.ra * P, cnt, ncclDouble, p.rank - 1, d->comm, c->stream);
+            if (r == ncclSuccess)
+                r = ncclRecv(a + (long)L.lo * P, cnt, ncclDouble, p.rank - 1, d->comm,
+                             c->stream);
+        }
+        if (r == ncclSuccess && p.rank < d->world - 1) {
+            const int g = L.hi - L.rb + 1;
+            const size_t cnt = (size_t)g * P;
+            r = ncclSend(a + (long)(L.rb - g) * P, cnt, ncclDouble, p.rank + 1, d->comm,
+                         c->stream);
+            if (r == ncclSuccess)
+                r = ncclRecv(a + (long)L.rb * P, cnt, ncclDouble, p.rank + 1, d->comm,
+                             c->stream);
+        }
     }
-    if (p.rank < d->world - 1) {
-        const int g = L.hi - L.rb + 1;
-        const size_t cnt = (size_t)g * P;
-        NCCLCHK(ncclSend(a + (long)(L.rb - g) * P, cnt, ncclDouble, p.rank + 1, d->comm,
-                         c->stream));
-        NCCLCHK(ncclRecv(a + (long)L.rb * P, cnt, ncclDouble, p.rank + 1, d->comm, c->stream));
-    }
-    NCCLCHK(ncclGroupEnd());
+    const ncclResult_t re = ncclGroupEnd();   // always close the group
+    if (r == ncclSuccess) r = re;
+    if (r != ncclSuccess)
+        return fail(MGX_E_RCCL, std::string("ghost exchange: ") + ncclGetErrorString(r));
     return MGX_OK;
 }
 
-static int exchange(mgx_ctx *c, int l, Field f) {
-    if (c->dist->world == 1) return MGX_OK;
+static int exchange(mgx_ctx *c, std::initializer_list<XF> xs) {
+    if (c->dist->world == 1 || xs.size() == 0) return MGX_OK;
     int rc = MGX_OK;
-    const PLevel &L = c->dist->parts[0].lv[l];
-    const double bytes = 16.0 * kGhost * L.pitch * c->dist->parts.size();
-    CHK(launch(c, MGX_K_HALO, l, bytes, [&] { rc = exchange_rows(c, l, f); }));
+    double bytes = 0;
+    for (const XF &x : xs)
+        bytes += 16.0 * (c->dist->parts[0].lv[x.l].ra - c->dist->parts[0].lv[x.l].lo) *
+                 c->dist->parts[0].lv[x.l].pitch * c->dist->parts.size();
+    CHK(launch(c, MGX_K_HALO, xs.begin()->l, bytes, [&] { rc = exchange_rows(c, xs); }));
     return rc;
 }
+
+static int exchange(mgx_ctx *c, int l, Field f) { return exchange(c, {XF{l, f}}); }
 
 // Restricted rhs of the first replicated level: every rank wrote its own rows
 // of the full array in its sub-context; make them whole everywhere.
@@ -291,8 +312,10 @@ static int smooth(mgx_ctx *c, int l, bool prolong, bool restrict_, bool norm) {
         const bool pr = prolong && first && !zero;
         const bool rs = restrict_ && last;
         const bool nm = norm && last && !rs;
-        if (!zero) CHK(exchange(c, l, kU));
-        if (pr && l + 1 < d->la) CHK(exchange(c, l + 1, kU));
+        if (!zero && pr && l + 1 < d->la)
+            CHK(exchange(c, {XF{l, kU}, XF{l + 1, kU}}));
+        else if (!zero)
+            CHK(exchange(c, l, kU));
         int mode = 0;
         if (zero) mode |= mgx::kModeZero;
         if (pr) mode |= mgx::kModeProlong;
@@ -381,8 +404,10 @@ static void dist_drop_spec(mgx_ctx *c) {
 // is made ready on level 1 and the per-rank norm sums are reduced by the caller.
 static int dist_cross(mgx_ctx *c, bool store_post) {
     Dist *d = c->dist;
-    CHK(exchange(c, 0, kU));
-    if (1 < d->la) CHK(exchange(c, 1, kU));
+    if (1 < d->la)
+        CHK(exchange(c, {XF{0, kU}, XF{1, kU}}));
+    else
+        CHK(exchange(c, 0, kU));
     for (auto &p : d->parts) {
         PLevel &L = p.lv[0];
         int P = -1, Q = -1;
