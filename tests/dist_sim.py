@@ -24,14 +24,15 @@ import torch.distributed as dist
 
 from oracle import oracle as O
 
-K_GHOST = 8   # dist.hip kGhost
+K_GHOST = 8         # dist.hip kGhost
+K_GHOST_FINE = 16   # dist.hip kGhostFine (level 0: the cross-cycle pass)
 
 
 class Block:
-    def __init__(self, n, ra, rb):
+    def __init__(self, n, ra, rb, ghost=K_GHOST):
         self.n, self.ra, self.rb = n, ra, rb
-        self.lo = max(0, ra - K_GHOST)
-        self.hi = min(n, rb - 1 + K_GHOST)
+        self.lo = max(0, ra - ghost)
+        self.hi = min(n, rb - 1 + ghost)
 
     def rows(self, a):
         return a.reshape(self.n + 1, self.n + 1)
@@ -70,7 +71,9 @@ class PartitionedVCycle:
         self.rank, self.world, self.N, self.L = rank, world, N, L
         self.dt, self.nu, self.nsmooth = dt, nu, nsmooth
         self.la = plan(0)[2]
-        self.blk = [Block(N >> l, *plan(l)[:2]) for l in range(self.la)]
+        self.blk = [Block(N >> l, *plan(l)[:2], K_GHOST_FINE if l == 0 else K_GHOST)
+                    for l in range(self.la)]
+        self.spec = False   # cross-cycle mode: next cycle's pre-smoothing already done
         self.v1 = [tower.level("v1", l) for l in range(L)]
         self.v2 = [tower.level("v2", l) for l in range(L)]
         self.u = [np.zeros((N >> l) ** 2 + 2 * (N >> l) + 1) for l in range(L)]
@@ -160,6 +163,60 @@ class PartitionedVCycle:
         dist.all_gather(parts, mine)
         for r, t in enumerate(parts):
             m[r * q:(r + 1) * q] = t.numpy()
+
+    def _restrict_owned(self, l):
+        """Residual of level l restricted into the owned rows of rhs[l+1]."""
+        n, b = self.N >> l, self.blk[l]
+        nc = n // 2
+        crs = O.restriction(self._res(l), n).reshape(nc + 1, nc + 1)
+        tgt = self.rhs[l + 1].reshape(nc + 1, nc + 1)
+        own = slice((b.ra + 1) // 2, (b.rb + 1) // 2)
+        tgt[own] = crs[own]
+
+    def _coarse_ready(self, l):
+        if l + 1 < self.la:
+            exchange(self.blk[l + 1], self.rhs[l + 1], self.rank, self.world)
+            return
+        self._gather_rhs(l + 1)
+
+    def _coarse_cycle(self, l):
+        if l < self.la:
+            self._level(l, True, False)
+        else:
+            self.u[l][:] = 0.0
+            self._full(l)
+
+    def vcycle_cross(self):
+        """dist.hip dist_vcycle with the cross-cycle pass on level 0: ONE u
+        ghost exchange (16 rows) feeds prolongation + post-smoothing + norm +
+        the next cycle's pre-smoothing + restriction."""
+        n, b = self.N, self.blk[0]
+        if not self.spec:   # first cycle: plain pre-smoothing pass
+            exchange(b, self.u[0], self.rank, self.world)
+            b.poison(self.u[0])
+            b.poison(self.rhs[0])
+            self._gs(0)
+            self._restrict_owned(0)
+            self._coarse_ready(0)
+        self._coarse_cycle(1)
+        exchange(b, self.u[0], self.rank, self.world)
+        if 1 < self.la:
+            exchange(self.blk[1], self.u[1], self.rank, self.world)
+            self.blk[1].poison(self.u[1])
+        b.poison(self.u[0])
+        b.poison(self.rhs[0])
+        self.u[0] += O.prolongation(self.u[1], n // 2)
+        self._gs(0)   # post-smoothing of this cycle
+        r = self._res(0).reshape(n + 1, n + 1)
+        i0, i1 = max(1, b.ra), min(n, b.rb)
+        part = torch.tensor([float(np.sum(r[i0:i1, 1:n] ** 2))], dtype=torch.float64)
+        dist.all_reduce(part)
+        self.u_post = self.owned(self.u[0]).copy()
+        self._gs(0)   # the next cycle's pre-smoothing, no exchange in between
+        self._restrict_owned(0)
+        self._coarse_ready(0)
+        self.spec = True
+        return math.sqrt(float(part[0]))
 
     def vcycle(self):
         """One V-cycle from u[0], rhs[0]; returns the all-reduced residual norm."""

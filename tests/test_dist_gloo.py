@@ -7,7 +7,9 @@
   exchanges over gloo send/recv, all-gather into the replicated levels,
   norm all-reduce) with the oracle's stencils and NaN-poisoned non-local
   rows: each rank's owned rows after two V-cycles are BITWISE the
-  single-process oracle's, and the all-reduced norm matches to 1e-12.
+  single-process oracle's, and the all-reduced norm matches to 1e-12;
+* the same for the cross-cycle schedule (one 16-row ghost exchange per cycle
+  on level 0; 14 rows pass, 12 fail -- the pass's cone).
 """
 import os
 import socket
@@ -25,7 +27,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, N, L, nsmooth, min_rows, q):
+def _worker(rank, world, port, N, L, nsmooth, min_rows, q, cross=False):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -56,16 +58,17 @@ def _worker(rank, world, port, N, L, nsmooth, min_rows, q):
                                 lambda l: mgd.partition(N, L, world, rank, l))
         sim.u[0][:] = u0
         sim.rhs[0] = O.compute_rhs(u0, N, v1, v2, dt, NU, 1.0 / N)
-        norms = [sim.vcycle() for _ in range(2)]
+        ncyc = 3 if cross else 2
+        norms = [sim.vcycle_cross() if cross else sim.vcycle() for _ in range(ncyc)]
         O.compute_rhs(tower.ufine, N, v1, v2, dt, NU, 1.0 / N, rhs=tower.rhsfine)
         ref_norms = []
-        for _ in range(2):
+        for _ in range(ncyc):
             tower.mg_inner(dt, NU, nsmooth=nsmooth)
             res = O.residual(tower.ufine, tower.rhsfine, N, v1, v2, dt, NU, 1.0 / N)
             ref_norms.append(O.compute_norm(res, N))
         ra, rb, la = mgd.partition(N, L, world, rank, 0)
         ref_rows = tower.ufine.reshape(N + 1, N + 1)[ra:rb]
-        got = sim.owned(sim.u[0])
+        got = sim.u_post if cross else sim.owned(sim.u[0])
         out.update(la=la, bitwise=bool(np.array_equal(got, ref_rows)),
                    finite=bool(np.isfinite(got).all()), norms=norms, ref_norms=ref_norms,
                    coarse_iters=sim.coarse_iters, ghost=K_GHOST)
@@ -77,11 +80,12 @@ def _worker(rank, world, port, N, L, nsmooth, min_rows, q):
         dist.destroy_process_group()
 
 
-def _run(world, N, L, nsmooth=3, min_rows=16):
+def _run(world, N, L, nsmooth=3, min_rows=16, cross=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, N, L, nsmooth, min_rows, q))
+    procs = [ctx.Process(target=_worker,
+                         args=(r, world, port, N, L, nsmooth, min_rows, q, cross))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -122,3 +126,15 @@ def test_partitioned_vcycle_gloo(world, N, L, min_rows):
 def test_partitioned_vcycle_gloo_nsmooth2():
     res = _run(2, 128, 4, nsmooth=2)
     assert all(res[r]["bitwise"] and res[r]["finite"] for r in range(2))
+
+
+@pytest.mark.parametrize("world,N,L", [(2, 128, 4), (4, 256, 4)])
+def test_partitioned_cross_cycle_gloo(world, N, L):
+    """The cross-cycle schedule on row blocks: one 16-row ghost exchange per
+    cycle feeds post-smoothing, norm and the next pre-smoothing (dist.hip
+    dist_cross); u_post after 3 cycles is bitwise the oracle's."""
+    res = _run(world, N, L, cross=True)
+    for r in range(world):
+        o = res[r]
+        assert o["finite"] and o["bitwise"], o
+        np.testing.assert_allclose(o["norms"], o["ref_norms"], rtol=1e-12)
