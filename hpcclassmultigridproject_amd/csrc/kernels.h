@@ -16,6 +16,7 @@ namespace mgx {
 // dgs = 1.0-4.0*rr*nu (gs.cpp:130, :75), drhs = 1.0+4.0*rr*nu (gs.cpp:44).
 struct Coef {
     double rr, nu, h, dgs, drhs, rdgs;   // rdgs = RN(1/dgs)
+    unsigned dsign;                       // sign bit of dgs (high-word position)
 };
 Coef make_coef(double k, double nu, double h);
 

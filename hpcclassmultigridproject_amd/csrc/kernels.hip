@@ -22,6 +22,7 @@ Coef make_coef(double k, double nu, double h) {
     c.dgs = 1.0 - 4.0 * c.rr * nu;       // gs.cpp:130 denominator, gs.cpp:75 diagonal
     c.drhs = 1.0 + 4.0 * c.rr * nu;      // gs.cpp:44
     c.rdgs = 1.0 / c.dgs;                // RN(1/d) for the Markstein division
+    c.dsign = std::signbit(c.dgs) ? 0x80000000u : 0u;
     return c;
 }
 
@@ -431,10 +432,17 @@ struct RowData {
     double2 r, x, y;
 };
 
+// The sign of a/d is sign(a) xor sign(d), also for a = +-0 (where the fma
+// chain alone would return +0 for a = -0): one v_xor + v_bfi on the high word
+// instead of a compare and two selects.
 __device__ __forceinline__ double div_diag(double a, const Coef &c) {
     const double q0 = a * c.rdgs;
     const double r = __builtin_fma(-q0, c.dgs, a);
-    return r == 0.0 ? q0 : __builtin_fma(r, c.rdgs, q0);
+    const double q = __builtin_fma(r, c.rdgs, q0);
+    const long long qb = __double_as_longlong(q);
+    const unsigned sh = (unsigned)(__double_as_longlong(a) >> 32) ^ c.dsign;
+    const unsigned qh = ((unsigned)(qb >> 32) & 0x7fffffffu) | (sh & 0x80000000u);
+    return __longlong_as_double(((long long)qh << 32) | (unsigned)qb);
 }
 // gs.cpp:130 with the Markstein division (bitwise equal to gs_point).
 __device__ __forceinline__ double gs_point_fast(double rhs, double v1, double v2, double uN,
@@ -710,17 +718,18 @@ struct WCfg {
     static constexpr int W = 2 * (64 - 2 * H);
 };
 
-// 64-bit value of lane l-1 (shr) / l+1 (shl); edge lanes get garbage-free 0
+// 64-bit value of lane l-1 (shr) / l+1 (shl); the edge lane reads 0
+// (bound_ctrl: one v_mov_b32_dpp per half, no zeroing move)
 __device__ __forceinline__ double dpp_shr1(double v) {
     const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x138, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x138, 0xf, 0xf, false);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, 0x138, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), 0x138, 0xf, 0xf, true);
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 __device__ __forceinline__ double dpp_shl1(double v) {
     const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x130, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x130, 0xf, 0xf, false);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, 0x130, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), 0x130, 0xf, 0xf, true);
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 // gs.cpp:130 / :75 with the velocity terms pre-scaled: t1 = v1*h/2, t2 = v2*h/2
