@@ -14,7 +14,8 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --outp
     -- python3 bench.py --steps 10 --warmup 2 --cpu-baseline off > "$OUT/bench_prof.log" 2>&1
 grep '^{' "$OUT/bench_prof.log" | tail -1 > "$OUT/bench.json"
 cp "$(find "$OUT/trace" -name 'run_kernel_stats.csv' | head -1)" "$OUT/kernel_stats.csv"
-bash tools/pmc_collect.sh "$OUT/pmc" 16384 9 3
+# same cycle pattern as the bench: one run_cycles(10) call
+bash tools/pmc_collect.sh "$OUT/pmc" 16384 9 10
 python3 tools/pmc_summary.py "$OUT/pmc" > "$OUT/pmc.json"
 python3 tools/hbm_traffic.py "$OUT/pmc.json" > "$OUT/hbm_traffic.json"
 rm -rf "$OUT/trace" "$OUT/pmc"
