@@ -18,6 +18,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 REF_PATH = os.path.join(HERE, "_ref", "libmgref.so")
+REF_NU2_PATH = os.path.join(HERE, "_ref", "libmgref_nu2.so")   # NITER = 2 (config 2)
 
 _dp = C.POINTER(C.c_double)
 
@@ -49,18 +50,25 @@ def lib():
     return _lib
 
 
-def ref_available() -> bool:
-    return os.path.exists(REF_PATH)
+def ref_available(nsmooth: int = 3) -> bool:
+    return os.path.exists(REF_NU2_PATH if nsmooth == 2 else REF_PATH)
 
 
-def ref():
+_refs = {}
+
+
+def ref(nsmooth: int = 3):
+    """The reference library (nsmooth 3 = unmodified; 2 = the NITER=2 build)."""
     global _ref
-    if _ref is None:
-        _ref = _load(REF_PATH)
-        _ref.ref_compute_norm.restype = C.c_double
-        _ref.ref_vcycle_once.restype = C.c_double
-        _ref.ref_time_vcycles.restype = C.c_double
-    return _ref
+    if nsmooth not in _refs:
+        r = _load(REF_NU2_PATH if nsmooth == 2 else REF_PATH)
+        r.ref_compute_norm.restype = C.c_double
+        r.ref_vcycle_once.restype = C.c_double
+        r.ref_time_vcycles.restype = C.c_double
+        _refs[nsmooth] = r
+    if nsmooth == 3:
+        _ref = _refs[3]
+    return _refs[nsmooth]
 
 
 D = C.c_double
@@ -178,10 +186,11 @@ class Tower:
 
 
 # ----------------------------------------------------------- reference (_ref)
-def ref_timestepper(u0, v1, v2, nu, maxlvl, n, dt, T, dx, tol=1e-6, shape=1, nthreads=1):
+def ref_timestepper(u0, v1, v2, nu, maxlvl, n, dt, T, dx, tol=1e-6, shape=1, nthreads=1,
+                    nsmooth=3):
     uT = np.empty_like(u0)
     a = [x.copy() for x in (u0, v1, v2)]
-    ref().ref_timestepper(_p(uT), _p(a[0]), _p(a[1]), _p(a[2]), D(nu), C.c_int(maxlvl),
+    ref(nsmooth).ref_timestepper(_p(uT), _p(a[0]), _p(a[1]), _p(a[2]), D(nu), C.c_int(maxlvl),
                           C.c_int(n), D(dt), D(T), D(dx), D(tol), C.c_int(shape),
                           C.c_int(nthreads))
     return uT

@@ -120,6 +120,36 @@ def vcycle_fixture(N, maxlvl, nthreads, tag, summary, keep_full=False):
     np.savez_compressed(os.path.join(HERE, f"vcycle_{tag}.npz"), **data)
 
 
+def config2_fixture(summary, nthreads=8):
+    """BASELINE configs[1]: N=4096, 3-level V-cycle, 2 pre/post RB-GS sweeps,
+    from the reference built with NITER=2 (oracle/Makefile libmgref_nu2.so):
+    one V-cycle and two timesteps (sha256 + stats, cycles per step)."""
+    N, maxlvl = 4096, 3
+    u0, v1, v2 = O.init_problem(N)
+    dx = 1.0 / N
+    dt = dx / 10
+    u = u0.copy()
+    t = time.time()
+    res = O.ref(2).ref_vcycle_once(p(u), p(v1), p(v2), I(N), I(maxlvl), D(dt), D(NU), I(1),
+                                   I(nthreads))
+    s = stats(u, N)
+    s.update({"maxlvl": maxlvl, "nsmooth": 2, "res_after": repr(res), "nthreads": nthreads,
+              "ref_seconds": round(time.time() - t, 2)})
+    summary["vcycle"]["N4096_L3_nu2"] = s
+    steps = 2
+    t = time.time()
+    uT = O.ref_timestepper(u0, v1, v2, NU, maxlvl, N, dt, steps * dt, dx, 1e-6, 1,
+                           nthreads=nthreads, nsmooth=2)
+    secs = time.time() - t
+    O.set_threads(nthreads)
+    uo, cyc = O.timestepper(u0, v1, v2, NU, maxlvl, N, dt, steps * dt, dx, nsmooth=2)
+    assert np.array_equal(uo, uT), "restatement differs from the NITER=2 reference"
+    s = stats(uT, N)
+    s.update({"maxlvl": maxlvl, "nsmooth": 2, "steps": steps, "cycles": list(cyc),
+              "nthreads": nthreads, "ref_seconds": round(secs, 1)})
+    summary["steps"]["N4096_L3_nu2_2steps"] = s
+
+
 def large_steps(N, maxlvl, steps, nthreads, summary):
     u0, v1, v2 = O.init_problem(N)
     dx = 1.0 / N
@@ -138,6 +168,8 @@ def large_steps(N, maxlvl, steps, nthreads, summary):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--large", action="store_true")
+    ap.add_argument("--only-config2", action="store_true",
+                    help="add the config-2 (NITER=2) fixtures to summary.json and stop")
     args = ap.parse_args()
     if not O.ref_available():
         sys.exit("oracle/_ref/libmgref.so missing: build with `make -C oracle` here")
@@ -147,6 +179,11 @@ def main():
     summary.setdefault("vcycle", {})
     summary.setdefault("steps", {})
     summary["generator"] = "tests/golden/make_golden.py (reference compiled by oracle/Makefile)"
+    if args.only_config2:
+        config2_fixture(summary)
+        with open(path, "w") as f:
+            json.dump(summary, f, indent=1, sort_keys=True)
+        return
     for N in (8, 16, 32, 64):
         ops_fixture(N)
     for N, nu, tag in ((32, NU, "N32"), (64, NU, "N64"), (128, NU, "N128"),
@@ -155,6 +192,7 @@ def main():
     vcycle_fixture(256, 4, 1, "N256_L4", summary, keep_full=True)
     vcycle_fixture(1024, 6, 8, "N1024_L6", summary)
     vcycle_fixture(4096, 3, 8, "N4096_L3", summary)
+    config2_fixture(summary)
     if args.large:
         vcycle_fixture(16384, 9, 8, "N16384_L9", summary)
         large_steps(16384, 9, 2, 8, summary)

@@ -193,3 +193,26 @@ def test_coarsest_solve_to_rounding_matches_direct_solve(N):
     err = np.max(np.abs(u[1:N, 1:N].ravel() - x)) / np.max(np.abs(x))
     assert err <= 1e-12, (err, iters)
     assert iters < 1000
+
+
+def test_config2_bitwise_vs_nu2_reference(golden_summary):
+    """BASELINE configs[1]: N=4096, 3-level V-cycle, 2 pre/post RB-GS sweeps
+    (coarsest n=1024 solved by GS to 1e-5) against the reference built with
+    NITER=2: one V-cycle and two Crank-Nicolson steps, sha256 + cycle counts."""
+    N, L = 4096, 3
+    dt = 1.0 / N / 10
+    u0, v1, v2 = init_problem(N)
+    sv = golden_summary["vcycle"]["N4096_L3_nu2"]
+    with Multigrid(N, L, dt, NU, nsmooth=2) as mg:
+        mg.upload(u0, v1, v2)
+        mg.rhs()
+        mg.mg_inner()
+        assert hashlib.sha256(mg.download().tobytes()).hexdigest() == sv["sha256"]
+        r = mg.residual_norm(0)
+        assert abs(r - float(sv["res_after"])) <= 1e-11 * float(sv["res_after"])
+    st = golden_summary["steps"]["N4096_L3_nu2_2steps"]
+    with Multigrid(N, L, dt, NU, nsmooth=2) as mg:
+        mg.upload(u0, v1, v2)
+        cyc = [mg.step(1e-6) for _ in range(st["steps"])]
+        assert cyc == st["cycles"]
+        assert hashlib.sha256(mg.download().tobytes()).hexdigest() == st["sha256"]
