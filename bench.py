@@ -16,7 +16,9 @@ scaling -- the same N=16384 grid row-partitioned over the ranks (libmgx RCCL
 halo exchange, replicated coarse levels), "scaling":
 "strong".  --weak instead doubles N (and adds a level) per 4x ranks, so the
 points per GPU stay within 2x of the 1-GPU run, "scaling": "weak"
-(configs[4], N=65536 on 8 GPUs: --N 65536 --levels 11).
+(configs[4], N=65536 on 8 GPUs: --N 65536 --levels 11; above N=16384 each
+rank initialises and uploads only its own rows, with the correct velocity
+tower, so no host or GPU ever holds the whole grid).
 roofline: the dominant kernel (largest device time: a finest-level fused
 smoothing pass) with achieved = its algorithmic bytes per launch (SURVEY 8d:
 40 B/point per RB sweep x 3 sweeps + the fused residual/restriction or
@@ -75,6 +77,8 @@ def parse():
     ap.add_argument("--weak", action="store_true",
                     help="multi-GPU: grow N with the GPU count (N*2 per 4x GPUs) instead of "
                          "partitioning the same grid")
+    ap.add_argument("--row-upload", choices=["auto", "on", "off"], default="auto",
+                    help="multi-GPU: each rank builds only its rows (auto: N > 16384)")
     ap.add_argument("--no-profile", action="store_true",
                     help="do not record per-kernel HIP events in the timed region")
     return ap.parse_args()
@@ -141,16 +145,26 @@ def main():
             N, L, g = 2 * N, L + 1, 4 * g
     nu = -4e-4
     dt = 1.0 / N / 10
-    u0, v1, v2 = pkg.init_problem(N, nthreads=16)
     dist_kw = {}
     if world > 1:
         from hpcclassmultigridproject_amd import dist as mgdist
         dist_kw = dict(world=world, rank=rank, unique_id=mgdist.broadcast_unique_id())
+    # row-block upload: each rank initialises and uploads only its rows (the
+    # whole grid never exists on one host/GPU: C5, N=65536 on 8 GPUs); it needs
+    # the correct velocity tower (the reference tower reads the whole grid)
+    row_upload = world > 1 and (args.row_upload == "on" or
+                                (args.row_upload == "auto" and N > 16384))
+    tower = pkg._lib.TOWER_CORRECT if row_upload else pkg._lib.TOWER_REFERENCE
     mg = pkg.Multigrid(N, L, dt, nu, nsmooth=args.nsmooth, device=local,
-                       smoother=args.smoother, fuse=args.fuse, **dist_kw)
+                       smoother=args.smoother, fuse=args.fuse, tower_mode=tower, **dist_kw)
     la = mg.dist_info()[2]
-    mg.upload(u0, v1, v2)
-    del u0, v1, v2
+    if row_upload:
+        lo, hi = mg.dist_rows(0)
+        mg.upload_rows([pkg.init_problem_rows(N, lo, hi + 1, nthreads=16)])
+    else:
+        u0, v1, v2 = pkg.init_problem(N, nthreads=16)
+        mg.upload(u0, v1, v2)
+        del u0, v1, v2
     mg.rhs()
     for _ in range(args.warmup):
         mg.run_cycles(1)
@@ -254,6 +268,7 @@ def main():
         "config": {"workload": f"N={N} fp64 V-cycle, L={L} (coarsest {N >> (L - 1)}), "
                                f"nu_smooth={args.nsmooth}, + residual/norm per step",
                    "N": N, "levels": L, "nsmooth": args.nsmooth,
+                   "tower": "correct (row-block upload)" if row_upload else "reference",
                    "parallelism": (f"row-partition x{world} on levels 0..{la - 1}, "
                                    f"levels {la}..{L - 1} replicated" if world > 1
                                    else "single"),

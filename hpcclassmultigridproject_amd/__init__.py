@@ -6,7 +6,8 @@ kernels in libmgx.so behind the C ABI of include/mgx.h.
 """
 from . import gs
 from ._lib import MGXError, Options, default_options, lib
-from .multigrid import Multigrid, default_maxlvl, init_problem, timestepper
+from .multigrid import (Multigrid, default_maxlvl, init_problem, init_problem_rows,
+                        timestepper)
 
 __all__ = ["gs", "MGXError", "Options", "default_options", "lib", "Multigrid",
-           "default_maxlvl", "init_problem", "timestepper"]
+           "default_maxlvl", "init_problem", "init_problem_rows", "timestepper"]

@@ -52,6 +52,7 @@ _SIGS = {
     "mgx_restriction": (_I, [_vp, _vp, _L]),
     "mgx_compute_rhs": (_I, [_vp, _vp, _L, _vp, _vp, _D, _D, _D]),
     "mgx_init_problem": (_I, [_vp, _vp, _vp, _L, _I]),
+    "mgx_init_problem_rows": (_I, [_vp, _vp, _vp, _L, _L, _L, _I]),
     "mgx_default_options": (None, [C.POINTER(Options)]),
     "mgx_timestepper": (_I, [_vp, _vp, _vp, _vp, _D, _I, _L, _D, _D, _D, _D, _I]),
     "mgx_timestepper_ex": (_I, [_vp, _vp, _vp, _vp, _D, _I, _L, _D, _D, _D, _D,
@@ -86,6 +87,8 @@ _SIGS = {
     "mgx_create_local_dist": (_I, [C.POINTER(_vp), _L, _I, _D, _D, C.POINTER(Options), _I]),
     "mgx_partition": (_I, [_L, _I, _I, _I, _I, C.POINTER(_I), C.POINTER(_I), C.POINTER(_I)]),
     "mgx_dist_info": (_I, [_vp, C.POINTER(_I), C.POINTER(_I), C.POINTER(_I)]),
+    "mgx_dist_rows": (_I, [_vp, _I, C.POINTER(_I), C.POINTER(_I)]),
+    "mgx_upload_rows": (_I, [_vp, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp)]),
     "mgx_get_tuning": (_I, [C.c_char_p, C.POINTER(_L)]),
 }
 

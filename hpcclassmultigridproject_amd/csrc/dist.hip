@@ -154,9 +154,16 @@ static int build_dist(mgx_ctx *c, int world, const std::vector<int> &ranks) {
 }
 
 // ---------------------------------------------------------------- transport
-enum Field { kU, kRhs };
+enum Field { kU, kRhs, kV1, kV2 };
 
-static double *field(const PLevel &L, Field f) { return f == kU ? L.U() : L.F(L.rhs); }
+static double *field(const PLevel &L, Field f) {
+    switch (f) {
+        case kU: return L.U();
+        case kRhs: return L.F(L.rhs);
+        case kV1: return L.F(L.v1);
+        default: return L.F(L.v2);
+    }
+}
 
 // Refresh the ghost rows of the listed (level, field)s from the neighbouring
 // ranks; over RCCL all of them go in ONE group (one latency, not one each).
@@ -632,6 +639,103 @@ int dist_download(mgx_ctx *c, double *u, hipMemcpyKind kind) {
     return rc;
 }
 
+// Row-block upload (no rank ever holds the whole grid): each part gets its
+// allocated rows [lo, hi] of u0 / v1 / v2 from the host, and the velocity
+// tower is built locally by injection (MGX_TOWER_CORRECT, each level from the
+// one above: coarse row I <- fine row 2I is owned by the same rank since row
+// blocks start at even rows), ghost rows exchanged per level; the first
+// replicated level is all-gathered and the sub-contexts inject the rest.
+// The boundary row n of v is never read by any operator and is not gathered.
+static int dist_upload_rows_impl(mgx_ctx *c, const double *const *u0s,
+                                 const double *const *v1s, const double *const *v2s) {
+    Dist *d = c->dist;
+    HIPCHK(hipSetDevice(c->device));
+    if (c->opt.tower_mode != MGX_TOWER_CORRECT)
+        return fail(MGX_E_ARG, "mgx_upload_rows: needs tower_mode MGX_TOWER_CORRECT (the "
+                               "reference tower mixes rows of the whole grid)");
+    if (d->la == 0) return fail(MGX_E_ARG, "mgx_upload_rows: no partitioned level, use mgx_upload");
+    const long w = c->N + 1;
+    for (size_t i = 0; i < d->parts.size(); ++i) {
+        if (!u0s || !v1s || !v2s || !u0s[i] || !v1s[i] || !v2s[i])
+            return fail(MGX_E_ARG, "mgx_upload_rows: null array");
+        Part &p = d->parts[i];
+        for (size_t l = 0; l < p.lv.size(); ++l) {
+            PLevel &L = p.lv[l];
+            for (double *b : {L.u[0], L.u[1], L.u[2], L.rhs})
+                if (b) HIPCHK(hipMemsetAsync(b, 0, L.bytes(), c->stream));
+            L.cur = 0;
+            L.spec = -1;
+            L.zero = false;
+        }
+        PLevel &L = p.lv[0];
+        const size_t row = w * sizeof(double), rows = L.hi - L.lo + 1;
+        HIPCHK(hipMemcpy2DAsync(L.u[0], L.pitch * sizeof(double), u0s[i], row, row, rows,
+                                hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpy2DAsync(L.v1, L.pitch * sizeof(double), v1s[i], row, row, rows,
+                                hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpy2DAsync(L.v2, L.pitch * sizeof(double), v2s[i], row, row, rows,
+                                hipMemcpyHostToDevice, c->stream));
+    }
+    // partitioned coarse levels: owned rows by injection, then ghost rows
+    for (int l = 1; l < d->la; ++l) {
+        for (auto &p : d->parts) {
+            PLevel &F = p.lv[l - 1], &C = p.lv[l];
+            for (int f = 0; f < 2; ++f) {
+                double *dst = (f ? C.F(C.v2) : C.F(C.v1)) + (long)C.ra * C.pitch;
+                const double *src = (f ? F.F(F.v2) : F.F(F.v1)) + 2L * C.ra * F.pitch;
+                mgx::launch_injection_rows(dst, C.pitch, src, F.pitch, C.rb - C.ra, C.n + 1,
+                                           c->stream);
+                CHK(check_launch("tower injection (rows)"));
+            }
+        }
+        CHK(exchange(c, {XF{l, kV1}, XF{l, kV2}}));
+    }
+    // first replicated level: owned rows into each sub-context, all-gathered
+    const long nl = c->N >> d->la, q = nl / d->world;
+    for (auto &p : d->parts) {
+        PLevel &F = p.lv[d->la - 1];
+        Level &S = p.sub->lv[0];
+        int ra, rb;
+        plan_rows(c->N, d->la, d->world, p.rank, &ra, &rb);
+        for (int f = 0; f < 2; ++f)
+            mgx::launch_injection_rows((f ? S.v2 : S.v1) + (long)ra * S.pitch, S.pitch,
+                                       (f ? F.F(F.v2) : F.F(F.v1)) + 2L * ra * F.pitch,
+                                       F.pitch, std::min<long>(rb, nl) - ra, nl + 1, c->stream);
+        CHK(check_launch("tower injection (replicated level)"));
+        for (auto &L : p.sub->lv) {
+            for (double *b : {L.u[0], L.u[1], L.rhs})
+                HIPCHK(hipMemsetAsync(b, 0, sizeof(double) * L.pitch * (L.n + 1), c->stream));
+            L.cur = 0;
+            L.spec = -1;
+            L.zero = false;
+        }
+    }
+    if (d->world > 1) {
+        for (int f = 0; f < 2; ++f) {
+            if (d->local) {
+                for (auto &dst : d->parts)
+                    for (auto &src : d->parts) {
+                        if (&dst == &src) continue;
+                        Level &Sd = dst.sub->lv[0], &Ss = src.sub->lv[0];
+                        const long off = (long)src.rank * q * Sd.pitch;
+                        HIPCHK(hipMemcpyAsync((f ? Sd.v2 : Sd.v1) + off, (f ? Ss.v2 : Ss.v1) + off,
+                                              sizeof(double) * q * Sd.pitch,
+                                              hipMemcpyDeviceToDevice, c->stream));
+                    }
+            } else {
+                Part &p = d->parts[0];
+                Level &S = p.sub->lv[0];
+                double *a = f ? S.v2 : S.v1;
+                NCCLCHK(ncclAllGather(a + (long)p.rank * q * S.pitch, a, (size_t)q * S.pitch,
+                                      ncclDouble, d->comm, c->stream));
+            }
+        }
+    }
+    for (auto &p : d->parts) CHK(build_tower(p.sub));   // correct mode: level by level
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return MGX_OK;
+}
+
 static int create_dist_common(mgx_ctx **out, long n, int maxlvl, double dt, double nu,
                               const mgx_options *opt, mgx_ctx **cp) {
     mgx_options o;
@@ -745,6 +849,22 @@ int mgx_create_local_dist(mgx_ctx **out, long n, int maxlvl, double dt, double n
     }
     *out = c;
     return MGX_OK;
+}
+
+int mgx_dist_rows(mgx_ctx *c, int part, int *lo, int *hi) {
+    if (!c || !c->dist || part < 0 || part >= (int)c->dist->parts.size() ||
+        c->dist->parts[part].lv.empty())
+        return fail(MGX_E_ARG, "mgx_dist_rows: not a partitioned context / bad part");
+    const PLevel &L = c->dist->parts[part].lv[0];
+    if (lo) *lo = L.lo;
+    if (hi) *hi = L.hi;
+    return MGX_OK;
+}
+
+int mgx_upload_rows(mgx_ctx *c, const double *const *u0, const double *const *v1,
+                    const double *const *v2) {
+    if (!c || !c->dist) return fail(MGX_E_ARG, "mgx_upload_rows: not a partitioned context");
+    return dist_upload_rows_impl(c, u0, v1, v2);
 }
 
 int mgx_dist_info(mgx_ctx *c, int *world, int *rank, int *replicated_level) {

@@ -33,6 +33,9 @@ void launch_raw_prolongation(double *up, const double *u, long n, hipStream_t s)
 // injection: dst[I*(m)+J] = src[2I*src_pitch + 2J], 0<=I,J<m; pitches in doubles
 void launch_injection(double *dst, long dst_pitch, const double *src, long src_pitch, long m,
                       hipStream_t s);
+// rows x cols block: dst[I*dst_pitch + J] = src[2I*src_pitch + 2J]
+void launch_injection_rows(double *dst, long dst_pitch, const double *src, long src_pitch,
+                           long rows, long cols, hipStream_t s);
 
 // Sum of squares of the interior of an (n+1)^2 field with row pitch `pitch`,
 // deterministic two-stage reduction; result written to *out (device) as sqrt.

@@ -196,6 +196,16 @@ __global__ __launch_bounds__(256) void k_injection(double *dst, long dpitch,
     dst[I * dpitch + J] = src[2 * I * spitch + 2 * J];
 }
 
+// Injection of a block of coarse rows: dst row I, col J <- src row 2I, col 2J.
+__global__ __launch_bounds__(256) void k_injection_rows(double *dst, long dpitch,
+                                                        const double *src, long spitch,
+                                                        long rows, long cols) {
+    const long I = blockIdx.y;
+    const long J = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (I >= rows || J >= cols) return;
+    dst[I * dpitch + J] = src[2 * I * spitch + 2 * J];
+}
+
 // Interior sum of squares, rows split over the grid; deterministic per block.
 __global__ __launch_bounds__(256) void k_norm_partial(const double *res, long n, long pitch,
                                                       int rows_per_block, double *partials) {
@@ -1597,6 +1607,13 @@ void launch_injection(double *dst, long dst_pitch, const double *src, long src_p
                       hipStream_t s) {
     dim3 g(cdiv(m, 256), (unsigned)m);
     MGX_LAUNCH(k_injection, g, dim3(256), s, dst, dst_pitch, src, src_pitch, m);
+}
+
+void launch_injection_rows(double *dst, long dst_pitch, const double *src, long src_pitch,
+                           long rows, long cols, hipStream_t s) {
+    if (rows <= 0 || cols <= 0) return;
+    dim3 g(cdiv(cols, 256), (unsigned)rows);
+    MGX_LAUNCH(k_injection_rows, g, dim3(256), s, dst, dst_pitch, src, src_pitch, rows, cols);
 }
 
 int norm_partials_size() { return kNormBlocks; }

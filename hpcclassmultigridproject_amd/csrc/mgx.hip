@@ -848,41 +848,59 @@ int mgx_timestepper(double *uT, const double *u0, const double *v1, const double
 
 // ---- reference problem setup (multigrid.cpp:206-233), host, glibc libm
 #include <thread>
-extern "C" int mgx_init_problem(double *u0, double *v1, double *v2, long N, int nthreads) {
-    if (!u0 || !v1 || !v2 || N < 1) return fail(MGX_E_ARG, "mgx_init_problem: bad args");
+// Rows [r0, r1) of the reference problem (multigrid.cpp:206-233) into arrays
+// holding just those rows; bitwise the rows of the full initialisation.
+static int init_rows(double *u0, double *v1, double *v2, long N, long r0, long r1,
+                     int nthreads) {
     const double PI = 3.1415926535897932;   // multigrid.cpp:14
     const double dx = 1.0 / N;
     const double x0 = 0.2, y0 = 0.4, sigma = 100.0, kx = 1.0 * PI, ky = 1.0 * PI;
     const long w = N + 1;
     int nt = nthreads > 0 ? nthreads : (int)std::thread::hardware_concurrency();
     if (nt < 1) nt = 1;
-    if (nt > w) nt = (int)w;
-    auto rows = [&](long r0, long r1) {
-        for (long i = r0; i < r1; ++i) {
+    if (nt > r1 - r0) nt = (int)std::max<long>(1, r1 - r0);
+    auto rows = [&](long a, long b) {
+        for (long i = a; i < b; ++i) {
             const double xi = (double)i;
+            const long o = (i - r0) * w;
             for (long j = 0; j < w; ++j) {
                 const double yj = (double)j;
-                u0[i * w + j] = std::exp(-sigma * ((xi * dx - x0) * (xi * dx - x0) +
-                                                   (yj * dx - y0) * (yj * dx - y0)));
-                v1[i * w + j] = -ky * std::sin(kx * xi * dx) * std::cos(ky * yj * dx);
-                v2[i * w + j] = kx * std::cos(kx * xi * dx) * std::sin(ky * yj * dx);
+                u0[o + j] = std::exp(-sigma * ((xi * dx - x0) * (xi * dx - x0) +
+                                               (yj * dx - y0) * (yj * dx - y0)));
+                v1[o + j] = -ky * std::sin(kx * xi * dx) * std::cos(ky * yj * dx);
+                v2[o + j] = kx * std::cos(kx * xi * dx) * std::sin(ky * yj * dx);
             }
         }
     };
     std::vector<std::thread> th;
-    const long per = (w + nt - 1) / nt;
+    const long per = (r1 - r0 + nt - 1) / nt;
     for (int t = 0; t < nt; ++t) {
-        long r0 = t * per, r1 = std::min(w, r0 + per);
-        if (r0 < r1) th.emplace_back(rows, r0, r1);
+        long a = r0 + t * per, b = std::min(r1, a + per);
+        if (a < b) th.emplace_back(rows, a, b);
     }
     for (auto &x : th) x.join();
-    for (long i = 0; i < N; ++i) {   // zero boundary, multigrid.cpp:227-233
-        u0[i] = 0.0;
-        u0[i * w + N] = 0.0;
-        u0[N * w + i + 1] = 0.0;
-        u0[i * w] = 0.0;
+    // zero boundary, multigrid.cpp:227-233 (row N, column 0 stays: the
+    // reference's loops skip that corner)
+    auto in = [&](long i) { return i >= r0 && i < r1; };
+    for (long i = 0; i < N; ++i) {
+        if (in(0)) u0[(0 - r0) * w + i] = 0.0;
+        if (in(i)) u0[(i - r0) * w + N] = 0.0;
+        if (in(N)) u0[(N - r0) * w + i + 1] = 0.0;
+        if (in(i)) u0[(i - r0) * w] = 0.0;
     }
     return MGX_OK;
+}
+
+extern "C" int mgx_init_problem(double *u0, double *v1, double *v2, long N, int nthreads) {
+    if (!u0 || !v1 || !v2 || N < 1) return fail(MGX_E_ARG, "mgx_init_problem: bad args");
+    return init_rows(u0, v1, v2, N, 0, N + 1, nthreads);
+}
+
+extern "C" int mgx_init_problem_rows(double *u0, double *v1, double *v2, long N, long r0,
+                                     long r1, int nthreads) {
+    if (!u0 || !v1 || !v2 || N < 1 || r0 < 0 || r1 > N + 1 || r0 >= r1)
+        return fail(MGX_E_ARG, "mgx_init_problem_rows: bad args");
+    return init_rows(u0, v1, v2, N, r0, r1, nthreads);
 }
 
 // ---- tuning knobs (process-wide)

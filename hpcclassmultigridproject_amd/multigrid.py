@@ -39,6 +39,15 @@ def init_problem(N: int, nthreads: int = 0):
     return u0, v1, v2
 
 
+def init_problem_rows(N: int, r0: int, r1: int, nthreads: int = 0):
+    """Rows [r0, r1) of init_problem(N): three (r1-r0)*(N+1) float64 arrays."""
+    cnt = (r1 - r0) * (N + 1)
+    u0, v1, v2 = (np.empty(cnt, dtype=np.float64) for _ in range(3))
+    check(lib().mgx_init_problem_rows(_np_ptr(u0), _np_ptr(v1), _np_ptr(v2), N, r0, r1,
+                                      nthreads))
+    return u0, v1, v2
+
+
 def timestepper(uT, u0, v1, v2, nu, maxlvl, n, dt, T, dx, tol, shape=1, *, nsmooth=3,
                 tower_mode=_lib.TOWER_REFERENCE, device=-1):
     """multigrid.cpp:124 -- run (int)(T/dt) CN steps; writes uT, returns cycles per step."""
@@ -118,6 +127,20 @@ class Multigrid:
         else:   # device tensors in the reference layout
             check(lib().mgx_upload_device(self._h, u0.data_ptr(), v1.data_ptr(),
                                           v2.data_ptr()))
+
+    def dist_rows(self, part=0):
+        """-> (lo, hi): allocated finest-level rows of local part `part`."""
+        lo, hi = C.c_int(), C.c_int()
+        check(lib().mgx_dist_rows(self._h, part, C.byref(lo), C.byref(hi)))
+        return lo.value, hi.value
+
+    def upload_rows(self, blocks):
+        """Row-block upload: blocks[i] = (u0, v1, v2) rows [lo, hi] of local part i
+        (init_problem_rows); needs tower_mode=TOWER_CORRECT."""
+        k = len(blocks)
+        arr = C.c_void_p * k
+        u, a, b = (arr(*[_np_ptr(blk[j]) for blk in blocks]) for j in range(3))
+        check(lib().mgx_upload_rows(self._h, u, a, b))
 
     def download(self, out=None):
         out = np.empty((self.N + 1) ** 2, dtype=np.float64) if out is None else out

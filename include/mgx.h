@@ -63,6 +63,10 @@ int mgx_compute_rhs(double *rhs, const double *u, long n, const double *v1,
  * v2 = pi cos(pi x) sin(pi y); x = i/N, y = j/N.  Arrays of (N+1)^2 doubles.
  * nthreads <= 0: all hardware threads. */
 int mgx_init_problem(double *u0, double *v1, double *v2, long N, int nthreads);
+/* Rows [r0, r1) only, into arrays of (r1-r0)*(N+1) doubles: bitwise those rows
+ * of mgx_init_problem (for row-block uploads, mgx_upload_rows). */
+int mgx_init_problem_rows(double *u0, double *v1, double *v2, long N, long r0, long r1,
+                          int nthreads);
 
 /* ---------------------------------------------------------------------------
  * Solver level.
@@ -220,6 +224,16 @@ int mgx_create_local_dist(mgx_ctx **out, long n, int maxlvl, double dt, double n
  * the first replicated level (levels >= it are whole on every rank). */
 int mgx_partition(long n, int maxlvl, int world, int rank, int level, int *ra, int *rb,
                   int *replicated_level);
+/* Allocated rows [*lo, *hi] (owned + ghosts) of the finest level of local part
+ * `part` (0 on an RCCL rank; 0..world-1 for mgx_create_local_dist). */
+int mgx_dist_rows(mgx_ctx *ctx, int part, int *lo, int *hi);
+/* Row-block upload, so that no rank ever holds the whole grid (SURVEY 8e C5:
+ * N=65536 on 8 GPUs): u0[i], v1[i], v2[i] hold rows [lo, hi] (mgx_dist_rows)
+ * of local part i, (hi-lo+1)*(N+1) doubles each.  The velocity tower is built
+ * on the device from the row blocks, which needs MGX_TOWER_CORRECT (the
+ * reference tower reads the whole grid).  Collective. */
+int mgx_upload_rows(mgx_ctx *ctx, const double *const *u0, const double *const *v1,
+                    const double *const *v2);
 /* world size, rank (-1 for a local multi-part context; 0/1 for single GPU),
  * first replicated level (maxlvl for a single-GPU context). */
 int mgx_dist_info(mgx_ctx *ctx, int *world, int *rank, int *replicated_level);

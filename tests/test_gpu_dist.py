@@ -220,3 +220,39 @@ def test_cross_cycle_partitioned_equals_single_N4096(G):
     assert p[4] == s[4]
     np.testing.assert_allclose(p[0] + [p[1], p[5], p[6]], s[0] + [s[1], s[5], s[6]],
                                rtol=NORM_RTOL)
+
+
+@pytest.mark.parametrize("N,L,G,min_rows", [(4096, 6, 4, 256), (1024, 6, 8, 16)],
+                         indirect=["min_rows"], ids=["N4096G4", "N1024G8"])
+def test_row_block_upload_equals_full_upload(N, L, G, min_rows):
+    """mgx_upload_rows: every part gets only its rows (init_problem_rows) and
+    the correct velocity tower is built on the device from the row blocks;
+    the solve is bitwise the single-GPU one with the correct tower."""
+    from hpcclassmultigridproject_amd import init_problem_rows
+    dt = 1.0 / N / 10
+    u0, v1, v2 = init_problem(N)
+    with Multigrid(N, L, dt, NU, tower_mode=_lib.TOWER_CORRECT) as mg:
+        mg.upload(u0, v1, v2)
+        mg.rhs()
+        n_ref = [mg.run_cycles(1) for _ in range(2)] + [mg.run_cycles(2)]
+        u_ref = mg.download()
+    with Multigrid(N, L, dt, NU, tower_mode=_lib.TOWER_CORRECT, local_parts=G) as mg:
+        blocks = []
+        for part in range(G):
+            lo, hi = mg.dist_rows(part)
+            blocks.append(init_problem_rows(N, lo, hi + 1))
+        mg.upload_rows(blocks)
+        mg.rhs()
+        n_got = [mg.run_cycles(1) for _ in range(2)] + [mg.run_cycles(2)]
+        u_got = mg.download()
+    assert np.array_equal(u_got, u_ref)
+    np.testing.assert_allclose(n_got, n_ref, rtol=NORM_RTOL)
+
+
+def test_row_block_upload_refuses_reference_tower():
+    with Multigrid(1024, 5, 1e-4, NU, local_parts=2) as mg:
+        lo, hi = mg.dist_rows(0)
+        from hpcclassmultigridproject_amd import init_problem_rows
+        blk = init_problem_rows(1024, lo, hi + 1)
+        with pytest.raises(MGXError):
+            mg.upload_rows([blk, blk])
