@@ -103,6 +103,9 @@ struct XArgs {
     int ra = 0, rb = -1, lo = 0, hi = -1;   // row block (rb < 0: whole level), as SmoothArgs
 };
 int launch_xsmooth(const XArgs &a, int sweeps, hipStream_t s);
+// Cross pass: 1 = interior strips run the unguarded march (default), 0 = all guarded.
+void set_xfast(long v);
+long get_xfast();
 // Levels with n <= tile_max_n use the 2-D tile form of the fused pass (small
 // levels: latency bound), larger ones the row march.  Default 2048, or the
 // MGX_TILE_MAX_N environment variable.

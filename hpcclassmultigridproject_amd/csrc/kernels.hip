@@ -10,6 +10,7 @@
 #include "kernels.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 namespace mgx {
@@ -977,15 +978,36 @@ struct XCfg {
     static constexpr int W = 2 * (64 - 2 * H);
     static constexpr int D = S + 2;              // B's lag in rows
     static constexpr int NU = 4, NRD = 8;        // LDS hand-off rings (rows)
+    // Rows an unguarded march may own: its warm-up reaches EA + EB + NR + D +
+    // S rows above its first owned row and its drain D + EB + NR + 5 below its
+    // last (B's garbage-in warm-up steps included), all of which must be rows
+    // in [1, n-1] so that no update ever lands on a Dirichlet row.
+    static constexpr int TOP = EA + EB + NR + D + S + 2, BOT = D + EB + NR + 6;
 };
 
-template <int WPB, int K>
+// Work of one k_xsmooth launch: up to 4 rectangles of (strip group, row)
+// units, enumerated group-major; pre[] are the prefix unit counts.
+struct XRegions {
+    int g0[4], g1[4], r0[4], r1[4];
+    long pre[5];
+    int count;
+};
+
+//
+// G = true: the guarded march (rows / columns may touch the Dirichlet
+// boundary; every stage tests them).  G = false: the unguarded march for
+// interior strips (every lane a column in [1, n-1]) on rows [TOP, n+1-BOT),
+// whose warm-up and drain stay in rows [1, n-1]: no per-stage predicates, so
+// no exec-mask branches, -26 % instructions.  They are separate kernels: one
+// function holding both marches compiled to a worse schedule than either
+// (3.6 ms vs 2.7 ms unguarded / 3.1 ms guarded at N=16384).
+template <int WPB, int K, bool G>
 __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     const double *__restrict__ uin, double *__restrict__ upost, double *__restrict__ upre,
     const double *__restrict__ rhs, const double *__restrict__ v1, const double *__restrict__ v2,
     const double *__restrict__ uc, long pitchc, double *__restrict__ rhsc,
-    double *__restrict__ partials, int n, long pitch, int groups, long units_per_wg, Coef c,
-    int ra, int rb, int lo, int hi, int store_post) {
+    double *__restrict__ partials, int n, long pitch, XRegions reg, long units_per_wg, Coef c,
+    int lo, int hi, int store_post) {
     using X = XCfg<K>;
     constexpr int S = X::S, H = X::H, NR = X::NR, W = X::W, D = X::D, NU = X::NU,
                   NRD = X::NRD, EA = X::EA, EB = X::EB;
@@ -997,21 +1019,17 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     const int wv = threadIdx.x >> 6;
     const bool isA = wv < WPB;   // wave-uniform role
     const int pr = isA ? wv : wv - WPB;
-    const int nrows = rb - ra;   // owned rows [ra, rb) (a row block on multi-GPU)
-    const long total = (long)groups * nrows;
+    const long total = reg.pre[reg.count];
     long start = (long)blockIdx.x * units_per_wg;
     const long end = min(total, start + units_per_wg);
     const int nc = n >> 1;
     const double hh = c.h * 0.5;
     double acc = 0.0;
 
-    while (start < end) {
-        const int grp = (int)(start / nrows);
-        const int a = ra + (int)(start % nrows);
-        const int b = (int)min((long)rb, (long)a + (end - start));
-        start += b - a;
-
-        const int j0 = (grp * WPB + pr) * W;
+    // One march of the pair over owned rows [a, b) of strip j0 (G: see above;
+    // the unguarded form keeps only the uniform owned-row tests of its outputs)
+    auto march = [&](const int j0, const int a, const int b) {
+        constexpr bool GM = G, GS = G, GN = G;   // make_u / stage / residual guards
         const int c0 = j0 - 2 * H + 2 * l;
         const bool act = c0 >= 0 && c0 <= n;
         const bool keep = act && l >= H && l < 64 - H;
@@ -1041,8 +1059,8 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
         auto make_u = [&](int R, const UPre &u, const bool odd) {
             double2 v = u.X;
             double2 pv;
-            const double q01 = j1 ? u.q01 : 0.0;
-            const double q11 = j1 ? u.q11 : 0.0;
+            const double q01 = (!GM || j1) ? u.q01 : 0.0;
+            const double q11 = (!GM || j1) ? u.q11 : 0.0;
             if (!odd) {
                 pv.x = u.q00;
                 pv.y = (u.q00 + q01) / 2;
@@ -1050,7 +1068,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                 pv.x = (u.q00 + u.q10) / 2;
                 pv.y = (u.q00 + u.q10 + q01 + q11) / 4;
             }
-            const bool on = act && R >= 0 && R <= n;
+            const bool on = !GM || (act && R >= 0 && R <= n);
             v.x = on ? v.x + pv.x : v.x;
             v.y = on ? v.y + pv.y : v.y;
             return v;
@@ -1061,6 +1079,32 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             const double2 x = ld2((v1 + o) + cl), y = ld2((v2 + o) + cl);
             d.x = make_double2(x.x * hh, x.y * hh);
             d.y = make_double2(y.x * hh, y.y * hh);
+        };
+        // one red-black stage h of the march step at row phase p on row r
+        auto stage = [&](double2 *ur, RowData *rd, const int p, const int h, const int r) {
+            const int iR = (p + 1 - h + 2 * NR) % NR;
+            const int iN = (p - h + 2 * NR) % NR;
+            const int iS = (p + 2 - h + 2 * NR) % NR;
+            const int cs = ((p + 1 - h) & 1) ^ (h & 1);
+            const RowData &d = rd[iR];
+            const bool inr = !GS || (r >= 1 && r <= n - 1);
+            // unguarded: a fresh (scalar) copy of nu per stage, so the compiler
+            // does not keep each point's four coefficients live across its three
+            // stages (that CSE needs ~50 more VGPRs than the 256 of two waves
+            // per SIMD: spills); guarded stages are branches, never CSE'd
+            Coef cg = c;
+            if (!GS) asm volatile("" : "+s"(cg.nu));
+            if (cs == 0) {
+                const double uW = dpp_shr1(ur[iR].y);
+                if (!GS || (inr && in0))
+                    ur[iR].x = gs_point_t(d.r.x, d.x.x, d.y.x, ur[iN].x, uW, ur[iS].x,
+                                          ur[iR].y, cg);
+            } else {
+                const double uE = dpp_shl1(ur[iR].x);
+                if (!GS || (inr && in1))
+                    ur[iR].y = gs_point_t(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x, ur[iS].y,
+                                          uE, cg);
+            }
         };
 
         // A's first step (aligned to NR so ring indices and parities are
@@ -1097,26 +1141,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                     ur[(p + 3) % NR] = make_u(s + 3, up[(p + 1) & 1], (p + 3) & 1);
                     load_u(s + 5, up[(p + 1) & 1]);
 #pragma unroll
-                    for (int h = 0; h < S; ++h) {
-                        const int r = s + 1 - h;
-                        const int iR = (p + 1 - h + 2 * NR) % NR;
-                        const int iN = (p - h + 2 * NR) % NR;
-                        const int iS = (p + 2 - h + 2 * NR) % NR;
-                        const int cs = ((p + 1 - h) & 1) ^ (h & 1);
-                        const RowData &d = rd[iR];
-                        const bool inr = r >= 1 && r <= n - 1;
-                        if (cs == 0) {
-                            const double uW = dpp_shr1(ur[iR].y);
-                            if (inr && in0)
-                                ur[iR].x = gs_point_t(d.r.x, d.x.x, d.y.x, ur[iN].x, uW,
-                                                      ur[iS].x, ur[iR].y, c);
-                        } else {
-                            const double uE = dpp_shl1(ur[iR].x);
-                            if (inr && in1)
-                                ur[iR].y = gs_point_t(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x,
-                                                      ur[iS].y, uE, c);
-                        }
-                    }
+                    for (int h = 0; h < S; ++h) stage(ur, rd, p, h, s + 1 - h);
                     // hand-off: rhs/v row s+1 (first used above), final u row s+2-S
                     {
                         const RowData &dh = rd[(p + 1) % NR];
@@ -1129,7 +1154,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         const int ro = s + 2 - S;
                         const double2 uf = ur[(p + 2 - S + 2 * NR) % NR];
                         uring[pr][ro & (NU - 1)][l] = uf;
-                        if (store_post && keep && ro >= a && ro < b)
+                        if (store_post && ro >= a && ro < b && keep)
                             st2((upost + (long)ro * pitch) + c0, uf);
                     }
                     load_rv(s + 3, rd[(p + 3) % NR]);
@@ -1161,45 +1186,39 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         const RowData &d = rd[iR];
                         const double uW = dpp_shr1(ur[iR].y);
                         const double uE = dpp_shl1(ur[iR].x);
-                        if (keep && r >= a && r < b && r >= 1 && r <= n - 1) {
-                            if (in0) {
-                                const double res = res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x,
-                                                               ur[iN].x, uW, ur[iS].x,
-                                                               ur[iR].y, c);
-                                acc += res * res;
-                            }
-                            if (in1) {
-                                const double res = res_point_t(d.r.y, d.x.y, d.y.y, ur[iR].y,
-                                                               ur[iN].y, ur[iR].x, ur[iS].y,
-                                                               uE, c);
-                                acc += res * res;
+                        if (r >= a && r < b) {
+                            if (GN) {
+                                if (keep && r >= 1 && r <= n - 1) {
+                                    if (in0) {
+                                        const double res =
+                                            res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x, ur[iN].x,
+                                                        uW, ur[iS].x, ur[iR].y, c);
+                                        acc += res * res;
+                                    }
+                                    if (in1) {
+                                        const double res =
+                                            res_point_t(d.r.y, d.x.y, d.y.y, ur[iR].y, ur[iN].y,
+                                                        ur[iR].x, ur[iS].y, uE, c);
+                                        acc += res * res;
+                                    }
+                                }
+                            } else {   // acc + 0.0 == acc (acc >= +0): selects, no branch
+                                const double r0 = res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x,
+                                                              ur[iN].x, uW, ur[iS].x, ur[iR].y,
+                                                              c);
+                                const double r1 = res_point_t(d.r.y, d.x.y, d.y.y, ur[iR].y,
+                                                              ur[iN].y, ur[iR].x, ur[iS].y, uE,
+                                                              c);
+                                acc += keep ? r0 * r0 : 0.0;
+                                acc += keep ? r1 * r1 : 0.0;
                             }
                         }
                     }
 #pragma unroll
-                    for (int h = 0; h < S; ++h) {
-                        const int r = s + 1 - h;
-                        const int iR = (q + 1 - h + 2 * NR) % NR;
-                        const int iN = (q - h + 2 * NR) % NR;
-                        const int iS = (q + 2 - h + 2 * NR) % NR;
-                        const int cs = ((q + 1 - h) & 1) ^ (h & 1);
-                        const RowData &d = rd[iR];
-                        const bool inr = r >= 1 && r <= n - 1;
-                        if (cs == 0) {
-                            const double uW = dpp_shr1(ur[iR].y);
-                            if (inr && in0)
-                                ur[iR].x = gs_point_t(d.r.x, d.x.x, d.y.x, ur[iN].x, uW,
-                                                      ur[iS].x, ur[iR].y, c);
-                        } else {
-                            const double uE = dpp_shl1(ur[iR].x);
-                            if (inr && in1)
-                                ur[iR].y = gs_point_t(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x,
-                                                      ur[iS].y, uE, c);
-                        }
-                    }
+                    for (int h = 0; h < S; ++h) stage(ur, rd, q, h, s + 1 - h);
                     {
                         const int ro = s + 2 - S;
-                        if (keep && ro >= a && ro < b)
+                        if (ro >= a && ro < b && keep)
                             st2((upre + (long)ro * pitch) + c0,
                                 ur[(q + 2 - S + 2 * NR) % NR]);
                     }
@@ -1210,8 +1229,8 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         const int iS = (q + 2 - S + 2 * NR) % NR;
                         const RowData &d = rd[iR];
                         const double uW = dpp_shr1(ur[iR].y);
-                        if (((q + 1 - S) & 1) == 0 && keep && r >= a && r < b && r >= 1 &&
-                            r <= n - 2 && in0 && c0 <= n - 2) {
+                        if (((q + 1 - S) & 1) == 0 && r >= a && r < b && keep &&
+                            (!GN || (r >= 1 && r <= n - 2 && in0 && c0 <= n - 2))) {
                             const double res = res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x,
                                                            ur[iN].x, uW, ur[iS].x, ur[iR].y, c);
                             (rhsc + (long)(r >> 1) * pitchc)[c0 >> 1] = res;
@@ -1223,6 +1242,18 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             }
         done_b:;
         }
+    };
+
+    while (start < end) {
+        int k = 0;
+        while (start >= reg.pre[k + 1]) ++k;
+        const long loc = start - reg.pre[k];
+        const int nr = reg.r1[k] - reg.r0[k];
+        const int grp = reg.g0[k] + (int)(loc / nr);
+        const int a = reg.r0[k] + (int)(loc % nr);
+        const int b = (int)min((long)reg.r1[k], (long)a + (end - start));
+        start += b - a;
+        march((grp * WPB + pr) * W, a, b);
     }
     if (!isA) {
         const double tot = wave_sum(acc);
@@ -1711,18 +1742,60 @@ static int smooth_winst(const SmoothArgs &A, hipStream_t s) {
     return (int)grid * WPB;   // NORM partials written
 }
 
-template <int WPB, int K>
-static int xsmooth_inst(const XArgs &A, hipStream_t s) {
-    constexpr int W = XCfg<K>::W;
-    static int slots = 0;
+long g_xfast = 1;   // cross pass: unguarded interior kernel (tuning key "xfast")
+void set_xfast(long v) { g_xfast = v; }
+long get_xfast() { return g_xfast; }
+
+template <int WPB, int K, bool G>
+static int xsmooth_slots() {
+    static int slots = 0;   // resident workgroups of this instantiation
     if (!slots) {
         int dev = 0, cus = 0, per = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_xsmooth<WPB, K>, 128 * WPB,
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_xsmooth<WPB, K, G>, 128 * WPB,
                                                            0);
         slots = std::max(1, cus) * std::max(1, per);
     }
+    return slots;
+}
+
+// One launch over `reg`; min_rows: the fewest rows per workgroup (each
+// workgroup's march pays a warm-up of ~EA + EB + D rows).  Returns the norm
+// partials written (grid * WPB) at `partials`.
+template <int WPB, int K, bool G>
+static int xsmooth_launch(const XArgs &A, const XRegions &reg, double *partials, int lo, int hi,
+                          long min_rows, long max_wgs, hipStream_t s) {
+    const long total = reg.pre[reg.count];
+    if (total <= 0) return 0;
+    long g = std::max<long>(1, std::min<long>(xsmooth_slots<WPB, K, G>(), total / min_rows));
+    g = std::min(g, max_wgs);
+    const long upw = (total + g - 1) / g;
+    const unsigned grid = (unsigned)((total + upw - 1) / upw);
+    MGX_LAUNCH((k_xsmooth<WPB, K, G>), dim3(grid), dim3(128 * WPB), s, A.uin, A.upost, A.upre,
+               A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch, reg, upw,
+               A.c, lo, hi, A.store_post ? 1 : 0);
+    return (int)grid * WPB;
+}
+
+static void add_region(XRegions &r, int g0, int g1, int r0, int r1) {
+    if (g1 <= g0 || r1 <= r0) return;
+    const int k = r.count++;
+    r.g0[k] = g0;
+    r.g1[k] = g1;
+    r.r0[k] = r0;
+    r.r1[k] = r1;
+    r.pre[k + 1] = r.pre[k] + (long)(g1 - g0) * (r1 - r0);
+}
+
+// The cross pass as two launches: the unguarded kernel over the interior
+// strip groups x rows [TOP, n+1-BOT), the guarded one over the rest (edge
+// groups, top / bottom bands: ~5 % of the points at N=16384), in short
+// segments so that it stays a small fraction of the pass.
+template <int WPB, int K>
+static int xsmooth_inst(const XArgs &A, hipStream_t s) {
+    using X = XCfg<K>;
+    constexpr int W = X::W, H = X::H;
     const long n = A.n;
     int ra = A.ra, rb = A.rb, lo = A.lo, hi = A.hi;
     if (rb < 0) {
@@ -1731,19 +1804,35 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
         lo = 0;
         hi = (int)n;
     }
-    const int groups = (int)((n + 1 + (long)W * WPB - 1) / ((long)W * WPB));
-    const long total = (long)groups * (rb - ra);
-    long g = std::max<long>(1, std::min<long>(slots, total / 64));
-    g = std::min<long>(g, kNormBlocks / WPB);
-    const long upw = (total + g - 1) / g;
-    const unsigned grid = (unsigned)((total + upw - 1) / upw);
 #ifdef MGX_PROBE_CLAMP
     lo = hi = 2;   // experiment build only: every load from one row (L2-resident)
 #endif
-    MGX_LAUNCH((k_xsmooth<WPB, K>), dim3(grid), dim3(128 * WPB), s, A.uin, A.upost, A.upre,
-               A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, A.partials, (int)n, A.pitch, groups,
-               upw, A.c, ra, rb, lo, hi, A.store_post ? 1 : 0);
-    return (int)grid * WPB;
+    const int groups = (int)((n + 1 + (long)W * WPB - 1) / ((long)W * WPB));
+    // interior groups: all WPB strips have every lane in columns [1, n-1]
+    int gi0 = 0, gi1 = -1;   // [gi0, gi1)
+    for (int g = 0; g < groups; ++g) {
+        const long c_first = (long)g * WPB * W - 2 * H;
+        const long c_last = ((long)g * WPB + WPB - 1) * W - 2 * H + 127;
+        if (c_first >= 1 && c_last <= n - 1) {
+            if (gi1 < 0) gi0 = g;
+            gi1 = g + 1;
+        }
+    }
+    const int ma = std::max(ra, X::TOP), mb = std::min(rb, (int)n + 1 - X::BOT);
+    XRegions inner{}, edge{};
+    if (g_xfast && gi1 > gi0 && mb > ma) {
+        add_region(inner, gi0, gi1, ma, mb);
+        add_region(edge, 0, gi0, ra, rb);
+        add_region(edge, gi1, groups, ra, rb);
+        add_region(edge, gi0, gi1, ra, ma);
+        add_region(edge, gi0, gi1, mb, rb);
+    } else {
+        add_region(edge, 0, groups, ra, rb);
+    }
+    const int cap = kNormBlocks / WPB / 2;
+    const int pm = xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, 64, cap, s);
+    const int pe = xsmooth_launch<WPB, K, true>(A, edge, A.partials + pm, lo, hi, 64, cap, s);
+    return pm + pe;
 }
 
 int launch_xsmooth(const XArgs &A, int sweeps, hipStream_t s) {

@@ -930,6 +930,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgxi::g_dist_min_rows = value;
         return MGX_OK;
     }
+    if (!strcmp(key, "xfast")) {
+        if (value != 0 && value != 1) return fail(MGX_E_ARG, "xfast must be 0 or 1");
+        mgx::set_xfast(value);
+        return MGX_OK;
+    }
     return fail(MGX_E_ARG, std::string("mgx_set_tuning: unknown key ") + key);
 }
 extern "C" int mgx_get_tuning(const char *key, long *value) {
@@ -953,6 +958,10 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "dist_min_rows")) {
         *value = mgxi::g_dist_min_rows;
+        return MGX_OK;
+    }
+    if (!strcmp(key, "xfast")) {
+        *value = mgx::get_xfast();
         return MGX_OK;
     }
     return fail(MGX_E_ARG, std::string("mgx_get_tuning: unknown key ") + key);
