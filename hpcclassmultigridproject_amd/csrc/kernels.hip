@@ -692,6 +692,31 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
     }
 }
 
+// Work of one march launch (k_wsmooth, k_xsmooth): up to 4 rectangles of
+// (strip group, row) units, enumerated group-major.  Region k covers strips
+// [sfirst, slim) in groups of WPB (the waves / pairs of a workgroup; those of a
+// last, partial group past slim idle) and rows [r0, r1); pre[] are the prefix
+// unit counts (groups x rows).
+struct MarchRegions {
+    int sfirst[4], slim[4], r0[4], r1[4];
+    long pre[5];
+    int count;
+};
+// -> (strip of wave / pair `w` of the group, a, b) of the segment starting at
+// unit `start` (at most `end`); strip < 0: this wave idles on the segment.
+__device__ __forceinline__ void region_segment(const MarchRegions &reg, int wpb, int w,
+                                               long start, long end, int &strip, int &a,
+                                               int &b) {
+    int k = 0;
+    while (start >= reg.pre[k + 1]) ++k;
+    const long loc = start - reg.pre[k];
+    const int nr = reg.r1[k] - reg.r0[k];
+    strip = reg.sfirst[k] + (int)(loc / nr) * wpb + w;
+    if (strip >= reg.slim[k]) strip = -1;
+    a = reg.r0[k] + (int)(loc % nr);
+    b = (int)min((long)reg.r1[k], (long)a + (end - start));
+}
+
 // k_wsmooth: the fused K-sweep pass of k_smooth as a WAVE-PRIVATE march.
 //
 // One workgroup = one wave of 64 lanes; lane l owns the column pair
@@ -727,6 +752,9 @@ struct WCfg {
     static constexpr int H = (E + 1) / 2;
     static constexpr int NR = S + 4;   // u ring = rhs/v ring = unroll period (even)
     static constexpr int W = 2 * (64 - 2 * H);
+    // rows an unguarded march may own: its warm-up updates rows down to
+    // E + NR + S - 2 above the first, its drain E - 2 below the last
+    static constexpr int TOP = E + NR + S + 2, BOT = E + 4;
 };
 
 // 64-bit value of lane l-1 (shr) / l+1 (shl); the edge lane reads 0
@@ -758,12 +786,14 @@ __device__ __forceinline__ double res_point_t(double rhs, double t1, double t2, 
     return rhs - (c.dgs * u + cc * uN + aa * uW + dd * uS + bb * uE);
 }
 
-template <int WPB, int K, int MODE>
+// G = false: the unguarded march (interior strips, rows [TOP, n+1-BOT) of
+// WCfg: no per-stage predicates), G = true: guarded (see k_xsmooth).
+template <int WPB, int K, int MODE, bool G>
 __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
     const double *__restrict__ uin, double *__restrict__ uout, const double *__restrict__ rhs,
     const double *__restrict__ v1, const double *__restrict__ v2, const double *__restrict__ uc,
     long pitchc, double *__restrict__ rhsc, double *__restrict__ partials, int n, long pitch,
-    int strips, long units_per_wg, Coef c, int ra, int rb, int lo, int hi) {
+    MarchRegions reg, long units_per_wg, Coef c, int lo, int hi) {
     using C = WCfg<K, MODE>;
     constexpr int S = C::S, E = C::E, H = C::H, NR = C::NR, W = C::W;
     // WPB waves per workgroup march WPB adjacent strips over the same rows,
@@ -771,8 +801,7 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
     // of the same rows, issued at about the same time
     const int l = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
-    const int nrows = rb - ra;
-    const long total = (long)strips * nrows;   // strips = strip GROUPS of WPB
+    const long total = reg.pre[reg.count];
     long start = (long)blockIdx.x * units_per_wg;
     const long end = min(total, start + units_per_wg);
     const int nc = n >> 1;
@@ -780,12 +809,12 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
     double acc = 0.0;
 
     while (start < end) {
-        const int strip = (int)(start / nrows);
-        const int a = ra + (int)(start % nrows);
-        const int b = (int)min((long)rb, (long)a + (end - start));
+        int strip, a, b;
+        region_segment(reg, WPB, wv, start, end, strip, a, b);
         start += b - a;
+        if (__builtin_amdgcn_readfirstlane(strip) < 0) continue;
 
-        const int j0 = (strip * WPB + wv) * W;
+        const int j0 = strip * W;
         const int c0 = j0 - 2 * H + 2 * l;
         const bool act = c0 >= 0 && c0 <= n;
         const bool keep = act && l >= H && l < 64 - H;
@@ -823,8 +852,8 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
             if (C::ZERO) v = make_double2(0.0, 0.0);
             if (C::PROL) {
                 double2 pr;
-                const double q01 = j1 ? u.q01 : 0.0;
-                const double q11 = j1 ? u.q11 : 0.0;
+                const double q01 = (!G || j1) ? u.q01 : 0.0;
+                const double q11 = (!G || j1) ? u.q11 : 0.0;
                 if (!odd) {
                     pr.x = u.q00;
                     pr.y = (u.q00 + q01) / 2;
@@ -832,7 +861,7 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                     pr.x = (u.q00 + u.q10) / 2;
                     pr.y = (u.q00 + u.q10 + q01 + q11) / 4;
                 }
-                const bool on = act && R >= 0 && R <= n;
+                const bool on = !G || (act && R >= 0 && R <= n);
                 v.x = on ? v.x + pr.x : v.x;
                 v.y = on ? v.y + pr.y : v.y;
             }
@@ -886,23 +915,27 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                     const int iS = (p + 2 - h + 2 * NR) % NR;
                     const int cs = ((p + 1 - h) & 1) ^ (h & 1);
                     const RowData &d = rd[iR];
-                    const bool inr = r >= 1 && r <= n - 1;
+                    const bool inr = !G || (r >= 1 && r <= n - 1);
+                    // unguarded: fresh scalar nu per stage (no cross-stage
+                    // coefficient CSE: it would need more VGPRs, see k_xsmooth)
+                    Coef cg = c;
+                    if (!G) asm volatile("" : "+s"(cg.nu));
                     if (cs == 0) {
                         const double uW = dpp_shr1(ur[iR].y);   // column c0-1
-                        if (inr && in0)
+                        if (!G || (inr && in0))
                             ur[iR].x = gs_point_t(d.r.x, d.x.x, d.y.x, ur[iN].x, uW, ur[iS].x,
-                                                  ur[iR].y, c);
+                                                  ur[iR].y, cg);
                     } else {
                         const double uE = dpp_shl1(ur[iR].x);   // column c0+2
-                        if (inr && in1)
+                        if (!G || (inr && in1))
                             ur[iR].y = gs_point_t(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x,
-                                                  ur[iS].y, uE, c);
+                                                  ur[iS].y, uE, cg);
                     }
                 }
                 // (3) row s+2-S is final
                 {
                     const int ro = s + 2 - S;
-                    if (keep && ro >= a && ro < b)
+                    if (ro >= a && ro < b && keep)
                         st2((uout + (long)ro * pitch) + c0, ur[(p + 2 - S + 2 * NR) % NR]);
                 }
                 // (4) residual stage on row s+1-S
@@ -914,15 +947,26 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                     const RowData &d = rd[iR];
                     const double uW = dpp_shr1(ur[iR].y);
                     if (C::REST) {
-                        if (((p + 1 - S) & 1) == 0 && keep && r >= a && r < b && r >= 1 &&
-                            r <= n - 2 && in0 && c0 <= n - 2) {
+                        if (((p + 1 - S) & 1) == 0 && r >= a && r < b && keep &&
+                            (!G || (r >= 1 && r <= n - 2 && in0 && c0 <= n - 2))) {
                             const double res = res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x,
                                                            ur[iN].x, uW, ur[iS].x, ur[iR].y, c);
                             (rhsc + (long)(r >> 1) * pitchc)[c0 >> 1] = res;
                         }
                     } else {
                         const double uE = dpp_shl1(ur[iR].x);
-                        if (keep && r >= a && r < b && r >= 1 && r <= n - 1) {
+                        if (!G) {   // acc + 0.0 == acc (acc >= +0): selects, no branch
+                            if (r >= a && r < b) {
+                                const double r0 = res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x,
+                                                              ur[iN].x, uW, ur[iS].x, ur[iR].y,
+                                                              c);
+                                const double r1 = res_point_t(d.r.y, d.x.y, d.y.y, ur[iR].y,
+                                                              ur[iN].y, ur[iR].x, ur[iS].y, uE,
+                                                              c);
+                                acc += keep ? r0 * r0 : 0.0;
+                                acc += keep ? r1 * r1 : 0.0;
+                            }
+                        } else if (keep && r >= a && r < b && r >= 1 && r <= n - 1) {
                             if (in0) {
                                 const double res = res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x,
                                                                ur[iN].x, uW, ur[iS].x,
@@ -985,13 +1029,6 @@ struct XCfg {
     static constexpr int TOP = EA + EB + NR + D + S + 2, BOT = D + EB + NR + 6;
 };
 
-// Work of one k_xsmooth launch: up to 4 rectangles of (strip group, row)
-// units, enumerated group-major; pre[] are the prefix unit counts.
-struct XRegions {
-    int g0[4], g1[4], r0[4], r1[4];
-    long pre[5];
-    int count;
-};
 
 //
 // G = true: the guarded march (rows / columns may touch the Dirichlet
@@ -1006,7 +1043,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     const double *__restrict__ uin, double *__restrict__ upost, double *__restrict__ upre,
     const double *__restrict__ rhs, const double *__restrict__ v1, const double *__restrict__ v2,
     const double *__restrict__ uc, long pitchc, double *__restrict__ rhsc,
-    double *__restrict__ partials, int n, long pitch, XRegions reg, long units_per_wg, Coef c,
+    double *__restrict__ partials, int n, long pitch, MarchRegions reg, long units_per_wg, Coef c,
     int lo, int hi, int store_post) {
     using X = XCfg<K>;
     constexpr int S = X::S, H = X::H, NR = X::NR, W = X::W, D = X::D, NU = X::NU,
@@ -1245,15 +1282,12 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     };
 
     while (start < end) {
-        int k = 0;
-        while (start >= reg.pre[k + 1]) ++k;
-        const long loc = start - reg.pre[k];
-        const int nr = reg.r1[k] - reg.r0[k];
-        const int grp = reg.g0[k] + (int)(loc / nr);
-        const int a = reg.r0[k] + (int)(loc % nr);
-        const int b = (int)min((long)reg.r1[k], (long)a + (end - start));
+        int strip, a, b;
+        region_segment(reg, WPB, pr, start, end, strip, a, b);
         start += b - a;
-        march((grp * WPB + pr) * W, a, b);
+        // a pair past its region's strips idles on the segment (A and B alike,
+        // so each pair's barrier count still matches between its two waves)
+        if (__builtin_amdgcn_readfirstlane(strip) >= 0) march(strip * W, a, b);
     }
     if (!isA) {
         const double tot = wave_sum(acc);
@@ -1717,34 +1751,87 @@ static int smooth_inst(const SmoothArgs &A, hipStream_t s) {
     return (int)grid;
 }
 
-template <int WPB, int K, int MODE>
-static int smooth_winst(const SmoothArgs &A, hipStream_t s) {
-    constexpr int W = WCfg<K, MODE>::W;
+long g_xfast = 1;   // unguarded interior march kernels (tuning key "xfast")
+void set_xfast(long v) { g_xfast = v; }
+long get_xfast() { return g_xfast; }
+
+template <int WPB>
+static void add_region(MarchRegions &r, int sfirst, int slim, int r0, int r1) {
+    if (slim <= sfirst || r1 <= r0) return;
+    const int k = r.count++;
+    r.sfirst[k] = sfirst;
+    r.slim[k] = slim;
+    r.r0[k] = r0;
+    r.r1[k] = r1;
+    r.pre[k + 1] = r.pre[k] + (long)((slim - sfirst + WPB - 1) / WPB) * (r1 - r0);
+}
+
+// Split a march over strips of width W (halo H pairs) and rows [ra, rb) into
+// the unguarded kernel's work -- interior strips (every lane a column in
+// [1, n-1]) x rows [TOP, n+1-BOT) -- and the guarded kernel's: the boundary
+// strips and the top / bottom bands (~1-2 % of the points).
+template <int WPB>
+static void march_regions(long n, int W, int H, int ra, int rb, int top, int bot, bool split,
+                          MarchRegions &inner, MarchRegions &edge) {
+    inner = MarchRegions{};
+    edge = MarchRegions{};
+    const int strips = (int)((n + 1 + W - 1) / W);
+    int si0 = strips, si1 = 0;   // interior strips [si0, si1)
+    for (int st = 0; st < strips; ++st) {
+        const long c_first = (long)st * W - 2 * H, c_last = c_first + 127;
+        if (c_first >= 1 && c_last <= n - 1) {
+            si0 = std::min(si0, st);
+            si1 = st + 1;
+        }
+    }
+    const int ma = std::max(ra, top), mb = std::min(rb, (int)n + 1 - bot);
+    if (split && si1 > si0 && mb > ma) {
+        add_region<WPB>(inner, si0, si1, ma, mb);
+        add_region<WPB>(edge, 0, si0, ra, rb);
+        add_region<WPB>(edge, si1, strips, ra, rb);
+        add_region<WPB>(edge, si0, si1, ra, ma);
+        add_region<WPB>(edge, si0, si1, mb, rb);
+    } else {
+        add_region<WPB>(edge, 0, strips, ra, rb);
+    }
+}
+
+template <int WPB, int K, int MODE, bool G>
+static int wsmooth_launch(const SmoothArgs &A, const MarchRegions &reg, double *partials,
+                          long max_wgs, hipStream_t s) {
+    const long total = reg.pre[reg.count];
+    if (total <= 0) return 0;
     static int slots = 0;   // resident workgroups of this instantiation
     if (!slots) {
         int dev = 0, cus = 0, per = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_wsmooth<WPB, K, MODE>,
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_wsmooth<WPB, K, MODE, G>,
                                                            64 * WPB, 0);
         slots = std::max(1, cus) * std::max(1, per);
     }
-    const long n = A.n;
-    const int groups = (int)((n + 1 + (long)W * WPB - 1) / ((long)W * WPB));
-    const long total = (long)groups * (A.rb - A.ra);
     long g = std::max<long>(1, std::min<long>(slots, total / 64));
-    g = std::min<long>(g, kNormBlocks / WPB);
+    g = std::min<long>(g, max_wgs);
     const long upw = (total + g - 1) / g;
     const unsigned grid = (unsigned)((total + upw - 1) / upw);
-    MGX_LAUNCH((k_wsmooth<WPB, K, MODE>), dim3(grid), dim3(64 * WPB), s, A.uin, A.uout, A.rhs,
-               A.v1, A.v2, A.uc, A.pitchc, A.rhsc, A.partials, (int)n, A.pitch, groups, upw,
-               A.c, A.ra, A.rb, A.lo, A.hi);
+    MGX_LAUNCH((k_wsmooth<WPB, K, MODE, G>), dim3(grid), dim3(64 * WPB), s, A.uin, A.uout,
+               A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch, reg, upw,
+               A.c, A.lo, A.hi);
     return (int)grid * WPB;   // NORM partials written
 }
 
-long g_xfast = 1;   // cross pass: unguarded interior kernel (tuning key "xfast")
-void set_xfast(long v) { g_xfast = v; }
-long get_xfast() { return g_xfast; }
+// One guarded launch over the whole level.  (The interior / edge split that
+// pays for k_xsmooth measured -5 % on the unguarded kernels of levels 1-2 and
+// +40 % for the edge launches: their passes are only ~300 rows per workgroup,
+// so the edge warm-ups do not amortise.)
+template <int WPB, int K, int MODE>
+static int smooth_winst(const SmoothArgs &A, hipStream_t s) {
+    using C = WCfg<K, MODE>;
+    MarchRegions inner, edge;
+    march_regions<WPB>(A.n, C::W, C::H, A.ra, A.rb, C::TOP, C::BOT, false, inner, edge);
+    return wsmooth_launch<WPB, K, MODE, true>(A, edge, A.partials, kNormBlocks / WPB, s);
+}
+
 
 template <int WPB, int K, bool G>
 static int xsmooth_slots() {
@@ -1764,7 +1851,7 @@ static int xsmooth_slots() {
 // workgroup's march pays a warm-up of ~EA + EB + D rows).  Returns the norm
 // partials written (grid * WPB) at `partials`.
 template <int WPB, int K, bool G>
-static int xsmooth_launch(const XArgs &A, const XRegions &reg, double *partials, int lo, int hi,
+static int xsmooth_launch(const XArgs &A, const MarchRegions &reg, double *partials, int lo, int hi,
                           long min_rows, long max_wgs, hipStream_t s) {
     const long total = reg.pre[reg.count];
     if (total <= 0) return 0;
@@ -1778,24 +1865,12 @@ static int xsmooth_launch(const XArgs &A, const XRegions &reg, double *partials,
     return (int)grid * WPB;
 }
 
-static void add_region(XRegions &r, int g0, int g1, int r0, int r1) {
-    if (g1 <= g0 || r1 <= r0) return;
-    const int k = r.count++;
-    r.g0[k] = g0;
-    r.g1[k] = g1;
-    r.r0[k] = r0;
-    r.r1[k] = r1;
-    r.pre[k + 1] = r.pre[k] + (long)(g1 - g0) * (r1 - r0);
-}
-
 // The cross pass as two launches: the unguarded kernel over the interior
-// strip groups x rows [TOP, n+1-BOT), the guarded one over the rest (edge
-// groups, top / bottom bands: ~5 % of the points at N=16384), in short
-// segments so that it stays a small fraction of the pass.
+// strips x rows [TOP, n+1-BOT), the guarded one over the rest (boundary
+// strips, top / bottom bands: ~1.7 % of the points at N=16384).
 template <int WPB, int K>
 static int xsmooth_inst(const XArgs &A, hipStream_t s) {
     using X = XCfg<K>;
-    constexpr int W = X::W, H = X::H;
     const long n = A.n;
     int ra = A.ra, rb = A.rb, lo = A.lo, hi = A.hi;
     if (rb < 0) {
@@ -1807,31 +1882,18 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
 #ifdef MGX_PROBE_CLAMP
     lo = hi = 2;   // experiment build only: every load from one row (L2-resident)
 #endif
-    const int groups = (int)((n + 1 + (long)W * WPB - 1) / ((long)W * WPB));
-    // interior groups: all WPB strips have every lane in columns [1, n-1]
-    int gi0 = 0, gi1 = -1;   // [gi0, gi1)
-    for (int g = 0; g < groups; ++g) {
-        const long c_first = (long)g * WPB * W - 2 * H;
-        const long c_last = ((long)g * WPB + WPB - 1) * W - 2 * H + 127;
-        if (c_first >= 1 && c_last <= n - 1) {
-            if (gi1 < 0) gi0 = g;
-            gi1 = g + 1;
-        }
-    }
-    const int ma = std::max(ra, X::TOP), mb = std::min(rb, (int)n + 1 - X::BOT);
-    XRegions inner{}, edge{};
-    if (g_xfast && gi1 > gi0 && mb > ma) {
-        add_region(inner, gi0, gi1, ma, mb);
-        add_region(edge, 0, gi0, ra, rb);
-        add_region(edge, gi1, groups, ra, rb);
-        add_region(edge, gi0, gi1, ra, ma);
-        add_region(edge, gi0, gi1, mb, rb);
-    } else {
-        add_region(edge, 0, groups, ra, rb);
-    }
-    const int cap = kNormBlocks / WPB / 2;
-    const int pm = xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, 64, cap, s);
-    const int pe = xsmooth_launch<WPB, K, true>(A, edge, A.partials + pm, lo, hi, 64, cap, s);
+    // inner: WPB pairs per workgroup, one workgroup per CU, long segments;
+    // edge: one pair per workgroup (4 per CU) and short segments, so that its
+    // ~44 K strip-rows at N=16384 (2 boundary strips + 71-row bands) take
+    // about one warm-up + 44 rows per workgroup
+    MarchRegions inner, edge, unused;
+    const bool split = g_xfast != 0;
+    march_regions<WPB>(n, X::W, X::H, ra, rb, X::TOP, X::BOT, split, inner, unused);
+    march_regions<1>(n, X::W, X::H, ra, rb, X::TOP, X::BOT, split, unused, edge);
+    const int pm = xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, 64,
+                                                 kNormBlocks / WPB / 2, s);
+    const int pe = xsmooth_launch<1, K, true>(A, edge, A.partials + pm, lo, hi, 32,
+                                              kNormBlocks / 2, s);
     return pm + pe;
 }
 
@@ -1919,7 +1981,7 @@ static int smooth_block(const SmoothArgs &A, hipStream_t s) {
             int dev = 0, cus = 0, per = 0;
             (void)hipGetDevice(&dev);
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_wsmooth<4, K, MODE>, 256,
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_wsmooth<4, K, MODE, false>, 256,
                                                                0);
             slots = std::max(1, cus) * std::max(1, per);
         }
