@@ -43,21 +43,31 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s HBM3E
 # (kind, level) -> kernel (template instance) of the default config, for the
 # PMC traffic summary committed under profiles/ (tools/profile_round.sh)
-KERNEL_IDS = {(8, 0): "mgx::k_xsmooth<4, 3>",
-              (0, 0): "mgx::k_wsmooth<4, 3, 4>",
-              (7, 0): "mgx::k_wsmooth<4, 3, 10>"}
+# (the cross pass is two launches: the unguarded interior kernel and the
+# guarded edge kernel; their traffic is summed)
+KERNEL_IDS = {(8, 0): ("mgx::k_xsmooth<4, 3, false>", "mgx::k_xsmooth<1, 3, true>"),
+              (0, 0): ("mgx::k_wsmooth<4, 3, 4, true>",),
+              (7, 0): ("mgx::k_wsmooth<4, 3, 10, true>",)}
 TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r1_hbm_traffic.json")
 
 
-def lookup_traffic(kname):
-    """HBM bytes per dispatch of the finest-level instance (largest grid) of kname."""
+def lookup_traffic(knames):
+    """HBM bytes per dispatch of the finest-level instances (largest traffic) of
+    the kernels in knames, summed (one launch of the op = one dispatch of each)."""
     if not os.path.exists(TRAFFIC_JSON):
         return None, None
-    best = None
-    for key, v in json.load(open(TRAFFIC_JSON))["kernels"].items():
-        if key.split(" grid=")[0] == kname and (best is None or v["hbm_bytes"] > best[1]):
-            best = (key, v["hbm_bytes"])
-    return best if best else (None, None)
+    kernels = json.load(open(TRAFFIC_JSON))["kernels"]
+    keys, total = [], 0.0
+    for kname in knames:
+        best = None
+        for key, v in kernels.items():
+            if key.split(" grid=")[0] == kname and (best is None or v["hbm_bytes"] > best[1]):
+                best = (key, v["hbm_bytes"])
+        if best is None:
+            return None, None
+        keys.append(best[0])
+        total += best[1]
+    return " + ".join(keys), total
 
 
 def parse():

@@ -69,6 +69,9 @@ __device__ __forceinline__ void st2(double *p, double2 v) {
 // Streaming (non-temporal) forms for data touched once per pass: the fused
 // smoother's rhs/v1/v2/u rows and its output rows.  MGX_NT=0 turns them into
 // plain accesses (A/B builds).
+#ifndef MGX_WSYNC
+#define MGX_WSYNC 0
+#endif
 #ifndef MGX_NT
 #define MGX_NT 1
 #endif
@@ -984,6 +987,11 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                 }
                 // (5) rhs/v row s+3 into the slot of row s+3-NR (dead)
                 load_rv(s + 3, rd[(p + 3) % NR]);
+#if MGX_WSYNC
+                // experiment: keep the WPB waves in step so the halo columns
+                // a neighbour loads are still in L2
+                if (MGX_WSYNC == 1 || (p & 1)) __builtin_amdgcn_s_barrier();
+#endif
                 if (++s > s_last) goto done;
             }
         }
@@ -2136,8 +2144,12 @@ void launch_coarse_solve(double *u, const double *rhs, const double *v1, const d
 // ---------------------------------------------------------------- probes
 // Streaming-bandwidth probes (the practical HBM ceiling SURVEY 8d asks for
 // beside the 8 TB/s spec): `nin` double2 input streams and one output stream,
-// 16 B per lane, grid-stride, out[i] = sum of the inputs.  nin = 1 is a copy;
-// nin = 4 is the smoother's stream shape (u, rhs, v1, v2 in, u out).
+// out[i] = sum of the inputs.  nin = 1 is a copy; nin = 4 is the smoother's
+// stream shape (u, rhs, v1, v2 in, u out).  The access shape is the best one
+// measured on the box (tools/probe/bw2.hip): one 16-B element per lane, one
+// workgroup per 4 KiB, non-temporal loads and stores -- 6.6 TB/s copy, 6.1 TB/s
+// 4-in/1-out, against 5.0-5.4 TB/s for grid-stride, per-workgroup chunks or
+// column-strip marches of the same bytes.
 template <int NIN>
 __global__ __launch_bounds__(256) void k_stream(const double2 *__restrict__ a,
                                                 const double2 *__restrict__ b,
@@ -2146,13 +2158,15 @@ __global__ __launch_bounds__(256) void k_stream(const double2 *__restrict__ a,
                                                 double2 *__restrict__ o, long n) {
     const long stride = (long)gridDim.x * blockDim.x;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        double2 v = a[i];
+        double2 v = ld2s(reinterpret_cast<const double *>(a + i));
         if (NIN > 1) {
-            const double2 y = b[i], z = c[i], w = d[i];
+            const double2 y = ld2s(reinterpret_cast<const double *>(b + i));
+            const double2 z = ld2s(reinterpret_cast<const double *>(c + i));
+            const double2 w = ld2s(reinterpret_cast<const double *>(d + i));
             v.x += y.x + z.x + w.x;
             v.y += y.y + z.y + w.y;
         }
-        o[i] = v;
+        st2s(reinterpret_cast<double *>(o + i), v);
     }
 }
 

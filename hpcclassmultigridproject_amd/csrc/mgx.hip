@@ -997,7 +997,8 @@ extern "C" int mgx_stream_bandwidth(long bytes_per_stream, int nin, int reps, do
         cleanup();
         return fail(MGX_E_HIP, "mgx_stream_bandwidth: stream/events");
     }
-    const int grid = std::max(1, cus) * 8;   // 8 workgroups (32 waves) per CU
+    // one 16-B element per lane (kernels.hip k_stream)
+    const int grid = (int)std::min<long>((n2 + 255) / 256, 1L << 30);
     double *a = buf[0], *b = buf[nin > 1 ? 1 : 0], *c = buf[nin > 1 ? 2 : 0],
            *d = buf[nin > 1 ? 3 : 0], *o = buf[nin];
     mgx::launch_stream(a, b, c, d, o, n2, nin, grid, s);   // warm-up
