@@ -1605,8 +1605,9 @@ __global__ __launch_bounds__(1024) void k_coarse_solve(double *u, const double *
     __shared__ double lds[16];
     __shared__ double s_norm;
     const int t = threadIdx.x;
-    const long m = n - 1;           // interior points per row
-    const long tot = m * m;
+    // 64 x 16 threads: lane tx walks the columns, ty the rows (no integer
+    // division in the loops: 64-bit div/mod is a long emulated sequence)
+    const int tx = t & 63, ty = t >> 6;
     if (zero_first) {
         for (long p = t; p < (long)(n + 1) * pitch; p += 1024) u[p] = 0.0;
         __syncthreads();
@@ -1615,23 +1616,25 @@ __global__ __launch_bounds__(1024) void k_coarse_solve(double *u, const double *
     double res = 1.0;
     while (it < maxit && res > tol) {
         for (int colour = 0; colour < 2; ++colour) {
-            for (long q = t; q < tot; q += 1024) {
-                const long i = 1 + q / m, j = 1 + q % m;
-                if (((i + j) & 1) != colour) continue;
-                const long p = i * pitch + j;
-                u[p] = gs_point(rhs[p], v1[p], v2[p], u[p - pitch], u[p - 1], u[p + pitch],
-                                u[p + 1], c);
+            for (int i = 1 + ty; i <= n - 1; i += 16) {
+                // first column of this colour in row i: (i + j) & 1 == colour
+                const int jc = 1 + ((i + 1 + colour) & 1);
+                for (int j = jc + 2 * tx; j <= n - 1; j += 128) {
+                    const long p = (long)i * pitch + j;
+                    u[p] = gs_point(rhs[p], v1[p], v2[p], u[p - pitch], u[p - 1], u[p + pitch],
+                                    u[p + 1], c);
+                }
             }
             __syncthreads();
         }
         double acc = 0.0;
-        for (long q = t; q < tot; q += 1024) {
-            const long i = 1 + q / m, j = 1 + q % m;
-            const long p = i * pitch + j;
-            const double r = res_point(rhs[p], v1[p], v2[p], u[p], u[p - pitch], u[p - 1],
-                                       u[p + pitch], u[p + 1], c);
-            acc += r * r;
-        }
+        for (int i = 1 + ty; i <= n - 1; i += 16)
+            for (int j = 1 + tx; j <= n - 1; j += 64) {
+                const long p = (long)i * pitch + j;
+                const double r = res_point(rhs[p], v1[p], v2[p], u[p], u[p - pitch], u[p - 1],
+                                           u[p + pitch], u[p + 1], c);
+                acc += r * r;
+            }
         double s = block_sum(acc, lds);
         if (t == 0) s_norm = sqrt(s);
         __syncthreads();

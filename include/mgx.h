@@ -169,7 +169,10 @@ int mgx_synchronize(mgx_ctx *ctx);
  * "march_kernel": row march on levels with n >= 4096: 1 wave-private
  * registers + DPP (default), 0 workgroup with an LDS ring (env MGX_MARCH_KERNEL).
  * "dist_min_rows": partitioned solvers replicate every level whose row blocks
- * would be shorter than this (default 256, even, >= 16); read at creation. */
+ * would be shorter than this (default 256, even, >= 16); read at creation.
+ * "xfast": 1 (default) runs the cross-cycle pass as an unguarded kernel over
+ * the interior strips and rows plus a guarded kernel over the boundary strips
+ * and bands; 0 = one guarded launch (bitwise the same results). */
 int mgx_set_tuning(const char *key, long value);
 int mgx_get_tuning(const char *key, long *value);
 

@@ -92,3 +92,33 @@ def test_run_cycles_batch_equals_single_calls(cross):
     (ua, ra, raa), (ub, rb, rab) = out
     assert np.array_equal(ua, ub)
     assert ra == rb and raa == rab
+
+
+def _cycles_plain(N, L, n, **kw):
+    u0, v1, v2 = init_problem(N)
+    with Multigrid(N, L, 1.0 / N / 10, NU, **kw) as mg:
+        mg.upload(u0, v1, v2)
+        mg.rhs()
+        norms = [mg.run_cycles(1) for _ in range(n)]
+        return mg.download(), norms
+
+
+@pytest.mark.parametrize("N,L,G", [(4096, 6, 1), (8192, 5, 1), (4096, 6, 4)],
+                         ids=["N4096", "N8192", "N4096_G4"])
+def test_unguarded_interior_kernel_equals_guarded(N, L, G, cross):
+    """Tuning key "xfast": 1 = the cross pass runs as the unguarded interior
+    kernel + the guarded edge kernel, 0 = one guarded launch over the level.
+    u bitwise, norms to the summation-order tolerance; also on row blocks
+    (virtual ranks, whose bands sit only at the first / last block)."""
+    cross(1)
+    old = _lib.get_tuning("xfast")
+    kw = dict(local_parts=G) if G > 1 else {}
+    try:
+        _lib.set_tuning("xfast", 0)
+        u0_, n0 = _cycles_plain(N, L, 3, **kw)
+        _lib.set_tuning("xfast", 1)
+        u1_, n1 = _cycles_plain(N, L, 3, **kw)
+    finally:
+        _lib.set_tuning("xfast", old)
+    assert np.array_equal(u0_, u1_)
+    np.testing.assert_allclose(n1, n0, rtol=NORM_RTOL)
