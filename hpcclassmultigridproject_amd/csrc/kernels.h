@@ -20,7 +20,8 @@ struct Coef {
 };
 Coef make_coef(double k, double nu, double h);
 
-inline long tower_pitch(long n) { return (n + 1 + 15) / 16 * 16; }
+// (+ MGX_PITCH_PAD extra doubles, a multiple of 16: row-pitch experiments)
+long tower_pitch(long n);
 
 // ---------------------------------------------------------------- reference layout
 void launch_raw_gs_colour(double *u, const double *rhs, const double *v1, const double *v2,
@@ -111,6 +112,16 @@ long get_xfast();
 // MGX_TILE_MAX_N environment variable.
 void set_tile_max_n(long v);
 long get_tile_max_n();
+// K = 3 tile passes on levels n >= tile32_min_n use 32 x 64 output tiles
+// (default: off), others 16 x 64; tile_xcd = 1 deals the tiles XCD-contiguous.
+void set_tile32_min_n(long v);
+long get_tile32_min_n();
+void set_tile_xcd(long v);
+long get_tile_xcd();
+// Row-march work order: bit 0 = band-major (neighbouring strip groups march
+// the same rows together), bit 1 = XCD-contiguous workgroup order.
+void set_march_order(long v);
+long get_march_order();
 // Workgroup width (lanes) of the row march on levels with n >= 4096: 128 or 256.
 void set_march_block(long v);
 void set_march_kernel(long v);

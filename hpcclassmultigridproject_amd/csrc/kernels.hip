@@ -15,6 +15,15 @@
 
 namespace mgx {
 
+long tower_pitch(long n) {
+    static long pad = -1;
+    if (pad < 0) {
+        const char *e = getenv("MGX_PITCH_PAD");
+        pad = e ? std::max(0L, atol(e) / 16 * 16) : 0;
+    }
+    return (n + 1 + 15) / 16 * 16 + pad;
+}
+
 Coef make_coef(double k, double nu, double h) {
     Coef c;
     c.rr = 0.5 * k / (h * h);            // gs.cpp:9-11
@@ -71,6 +80,9 @@ __device__ __forceinline__ void st2(double *p, double2 v) {
 // plain accesses (A/B builds).
 #ifndef MGX_WSYNC
 #define MGX_WSYNC 0
+#endif
+#ifndef MGX_XPRIO
+#define MGX_XPRIO 0   // experiment: s_setprio 1 for the B (1) / A (2) waves of k_xsmooth
 #endif
 #ifndef MGX_NT
 #define MGX_NT 1
@@ -699,11 +711,18 @@ __global__ __launch_bounds__(BLOCK) void k_smooth(
 // (strip group, row) units, enumerated group-major.  Region k covers strips
 // [sfirst, slim) in groups of WPB (the waves / pairs of a workgroup; those of a
 // last, partial group past slim idle) and rows [r0, r1); pre[] are the prefix
-// unit counts (groups x rows).
+// unit counts (groups x rows).  band[k] > 0: the region is enumerated
+// band-major instead -- bands of band[k] rows, group-major inside a band --
+// so that with band[k] = units per workgroup, workgroup (band b, group j)
+// marches rows [r0 + b*band, +band) of group j and the workgroups of
+// neighbouring groups march the same rows at the same time.  xcd = 1: the
+// workgroup order is dealt XCD-contiguous (wg_order).
 struct MarchRegions {
     int sfirst[4], slim[4], r0[4], r1[4];
+    int band[4];
     long pre[5];
     int count;
+    int xcd;
 };
 // -> (strip of wave / pair `w` of the group, a, b) of the segment starting at
 // unit `start` (at most `end`); strip < 0: this wave idles on the segment.
@@ -712,12 +731,32 @@ __device__ __forceinline__ void region_segment(const MarchRegions &reg, int wpb,
                                                int &b) {
     int k = 0;
     while (start >= reg.pre[k + 1]) ++k;
-    const long loc = start - reg.pre[k];
-    const int nr = reg.r1[k] - reg.r0[k];
+    long loc = start - reg.pre[k];
+    int r0 = reg.r0[k], nr = reg.r1[k] - reg.r0[k];
+    if (reg.band[k] > 0) {   // band-major: (band, group, row)
+        const int ng = (reg.slim[k] - reg.sfirst[k] + wpb - 1) / wpb;
+        const long per = (long)ng * reg.band[k];
+        const int bi = (int)(loc / per);
+        loc -= bi * per;
+        r0 += bi * reg.band[k];
+        nr = min(reg.band[k], nr - bi * reg.band[k]);
+    }
     strip = reg.sfirst[k] + (int)(loc / nr) * wpb + w;
     if (strip >= reg.slim[k]) strip = -1;
-    a = reg.r0[k] + (int)(loc % nr);
-    b = (int)min((long)reg.r1[k], (long)a + (end - start));
+    a = r0 + (int)(loc % nr);
+    b = (int)min((long)(r0 + nr), (long)a + (end - start));
+}
+
+// Logical workgroup index of a march launch.  Workgroups are dealt
+// round-robin over the 8 XCDs (b and b+8 share one, MI355X_MICROARCH
+// "Workgroup dispatch"); reg.xcd = 1 gives each XCD a contiguous run of
+// logical indices -- neighbouring strip groups of a band -- so the halo
+// columns two neighbours both read are fetched once into that XCD's L2.
+__device__ __forceinline__ long wg_order(const MarchRegions &reg) {
+    const int b = blockIdx.x;
+    if (!reg.xcd) return b;
+    const int G = gridDim.x, q = G >> 3, r = G & 7, x = b & 7;
+    return (long)x * q + min(x, r) + (b >> 3);
 }
 
 // k_wsmooth: the fused K-sweep pass of k_smooth as a WAVE-PRIVATE march.
@@ -805,7 +844,7 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
     const int l = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     const long total = reg.pre[reg.count];
-    long start = (long)blockIdx.x * units_per_wg;
+    long start = wg_order(reg) * units_per_wg;
     const long end = min(total, start + units_per_wg);
     const int nc = n >> 1;
     const double hh = c.h * 0.5;
@@ -1064,8 +1103,13 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     const int wv = threadIdx.x >> 6;
     const bool isA = wv < WPB;   // wave-uniform role
     const int pr = isA ? wv : wv - WPB;
+#if MGX_XPRIO == 1
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 64 * WPB) __builtin_amdgcn_s_setprio(1);
+#elif MGX_XPRIO == 2
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) < 64 * WPB) __builtin_amdgcn_s_setprio(1);
+#endif
     const long total = reg.pre[reg.count];
-    long start = (long)blockIdx.x * units_per_wg;
+    long start = wg_order(reg) * units_per_wg;
     const long end = min(total, start + units_per_wg);
     const int nc = n >> 1;
     const double hh = c.h * 0.5;
@@ -1312,10 +1356,10 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
 // by one point per stage, so the output tile is exact (same argument as
 // k_smooth).  Each lane owns fixed column pairs of the tile and keeps their
 // rhs / v1 / v2 in registers for all stages.
-template <int K, int MODE>
+template <int K, int MODE, int TRV = 16>
 struct TileCfg {
     using C = SmoothCfg<K, MODE>;
-    static constexpr int TR = 16, TC = 64;               // output tile
+    static constexpr int TR = TRV, TC = 64;              // output tile
     static constexpr int EH = (C::E + 1) / 2 * 2;         // halo, even
     static constexpr int RT = TR + 2 * EH, WT = TC + 2 * EH;
     static constexpr int PAIRS = RT * WT / 2;
@@ -1323,19 +1367,24 @@ struct TileCfg {
     static constexpr int PPT = (PAIRS + THREADS - 1) / THREADS;   // pairs per thread
 };
 
-template <int K, int MODE>
+template <int K, int MODE, int TRV>
 __global__ __launch_bounds__(256) void k_smooth_tile(
     const double *__restrict__ uin, double *__restrict__ uout, const double *__restrict__ rhs,
     const double *__restrict__ v1, const double *__restrict__ v2, const double *__restrict__ uc,
     long pitchc, double *__restrict__ rhsc, double *__restrict__ partials, int n, long pitch,
-    int tiles_x, Coef c, int ra, int rb, int lo, int hi) {
+    int tiles_x, Coef c, int ra, int rb, int lo, int hi, int xcd) {
     using C = SmoothCfg<K, MODE>;
-    using T = TileCfg<K, MODE>;
+    using T = TileCfg<K, MODE, TRV>;
     constexpr int S = C::S, EH = T::EH, WT = T::WT, PPT = T::PPT, HW = WT / 2;
     __shared__ __attribute__((aligned(16))) double tu[T::RT * WT];
 
     const int t = threadIdx.x;
-    const int ty = blockIdx.x / tiles_x, tx = blockIdx.x % tiles_x;
+    int bid = blockIdx.x;
+    if (xcd) {   // XCD-contiguous tile order (see wg_order): neighbours' halos share an L2
+        const int G = gridDim.x, q = G >> 3, r = G & 7, x = bid & 7;
+        bid = x * q + min(x, r) + (bid >> 3);
+    }
+    const int ty = bid / tiles_x, tx = bid % tiles_x;
     const long i0 = ra + (long)ty * T::TR - EH, j0 = (long)tx * T::TC - EH;   // tile origin (even)
     const int nc = n >> 1;
 
@@ -1440,7 +1489,7 @@ __global__ __launch_bounds__(256) void k_smooth_tile(
     if (C::NORM) {
         __shared__ double red_lds[4];
         const double tot = block_sum(acc, red_lds);
-        if (t == 0) partials[blockIdx.x] = tot;
+        if (t == 0) partials[bid] = tot;
     }
 }
 
@@ -1807,6 +1856,28 @@ static void march_regions(long n, int W, int H, int ra, int rb, int top, int bot
     }
 }
 
+long g_march_order = -1;   // tuning key "march_order": bit 0 bands, bit 1 XCD order
+static long march_order() {
+    if (g_march_order < 0) {
+        const char *e = getenv("MGX_MARCH_ORDER");
+        g_march_order = e ? atol(e) : 0;
+    }
+    return g_march_order;
+}
+void set_march_order(long v) { g_march_order = v; }
+long get_march_order() { return march_order(); }
+
+// The work order of a launch of `upw` units per workgroup (march_order):
+// band-major with bands of upw rows on a one-region launch, and/or the
+// XCD-contiguous workgroup order.  Only the order changes, not the work.
+static MarchRegions order_regions(const MarchRegions &reg, long upw) {
+    MarchRegions r = reg;
+    const long m = march_order();
+    if ((m & 1) && r.count == 1 && upw < r.r1[0] - r.r0[0]) r.band[0] = (int)upw;
+    if (m & 2) r.xcd = 1;
+    return r;
+}
+
 template <int WPB, int K, int MODE, bool G>
 static int wsmooth_launch(const SmoothArgs &A, const MarchRegions &reg, double *partials,
                           long max_wgs, hipStream_t s) {
@@ -1826,8 +1897,8 @@ static int wsmooth_launch(const SmoothArgs &A, const MarchRegions &reg, double *
     const long upw = (total + g - 1) / g;
     const unsigned grid = (unsigned)((total + upw - 1) / upw);
     MGX_LAUNCH((k_wsmooth<WPB, K, MODE, G>), dim3(grid), dim3(64 * WPB), s, A.uin, A.uout,
-               A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch, reg, upw,
-               A.c, A.lo, A.hi);
+               A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch,
+               order_regions(reg, upw), upw, A.c, A.lo, A.hi);
     return (int)grid * WPB;   // NORM partials written
 }
 
@@ -1871,8 +1942,8 @@ static int xsmooth_launch(const XArgs &A, const MarchRegions &reg, double *parti
     const long upw = (total + g - 1) / g;
     const unsigned grid = (unsigned)((total + upw - 1) / upw);
     MGX_LAUNCH((k_xsmooth<WPB, K, G>), dim3(grid), dim3(128 * WPB), s, A.uin, A.upost, A.upre,
-               A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch, reg, upw,
-               A.c, lo, hi, A.store_post ? 1 : 0);
+               A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch,
+               order_regions(reg, upw), upw, A.c, lo, hi, A.store_post ? 1 : 0);
     return (int)grid * WPB;
 }
 
@@ -1953,18 +2024,49 @@ static long tile_max_n() {
 
 long get_tile_max_n() { return tile_max_n(); }
 
-template <int K, int MODE>
-static int smooth_tile_inst(const SmoothArgs &A, hipStream_t s) {
-    using T = TileCfg<K, MODE>;
+long g_tile32_min_n = -1;   // 32-row tiles on levels n >= this (tuning key "tile32_min_n")
+long g_tile_xcd = -1;       // XCD-contiguous tile order (tuning key "tile_xcd")
+
+static long tile32_min_n() {
+    if (g_tile32_min_n < 0) {
+        const char *e = getenv("MGX_TILE32_MIN_N");
+        g_tile32_min_n = e ? atol(e) : (1L << 30);
+    }
+    return g_tile32_min_n;
+}
+void set_tile32_min_n(long v) { g_tile32_min_n = v; }
+long get_tile32_min_n() { return tile32_min_n(); }
+static long tile_xcd() {
+    if (g_tile_xcd < 0) {
+        const char *e = getenv("MGX_TILE_XCD");
+        g_tile_xcd = e ? atol(e) : 0;
+    }
+    return g_tile_xcd;
+}
+void set_tile_xcd(long v) { g_tile_xcd = v; }
+long get_tile_xcd() { return tile_xcd(); }
+
+template <int K, int MODE, int TRV>
+static int smooth_tile_rows(const SmoothArgs &A, hipStream_t s) {
+    using T = TileCfg<K, MODE, TRV>;
     const long n = A.n;
     const int tiles_x = (int)((n + 1 + T::TC - 1) / T::TC);
     const int tiles_y = (int)((A.rb - A.ra + T::TR - 1) / T::TR);
     const long grid = (long)tiles_x * tiles_y;
     if ((MODE & 8) && grid > kNormBlocks) return -1;
-    MGX_LAUNCH((k_smooth_tile<K, MODE>), dim3((unsigned)grid), dim3(256), s, A.uin, A.uout,
-               A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, A.partials, (int)n, A.pitch, tiles_x,
-               A.c, A.ra, A.rb, A.lo, A.hi);
+    MGX_LAUNCH((k_smooth_tile<K, MODE, TRV>), dim3((unsigned)grid), dim3(256), s, A.uin,
+               A.uout, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, A.partials, (int)n, A.pitch,
+               tiles_x, A.c, A.ra, A.rb, A.lo, A.hi, tile_xcd() ? 1 : 0);
     return (int)grid;
+}
+
+// 16 x 64 output tiles (halo overhead 2.5x the tile); with K = 3 on levels
+// n >= tile32_min_n, 32 x 64 (1.9x, more work per workgroup)
+template <int K, int MODE>
+static int smooth_tile_inst(const SmoothArgs &A, hipStream_t s) {
+    if constexpr (K == 3)
+        if (A.n >= tile32_min_n()) return smooth_tile_rows<K, MODE, 32>(A, s);
+    return smooth_tile_rows<K, MODE, 16>(A, s);
 }
 
 long g_march_block = -1;   // workgroup width of the row march for n >= 4096

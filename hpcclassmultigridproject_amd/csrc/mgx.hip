@@ -935,6 +935,21 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgx::set_xfast(value);
         return MGX_OK;
     }
+    if (!strcmp(key, "tile32_min_n")) {
+        if (value < 0) return fail(MGX_E_ARG, "tile32_min_n must be >= 0");
+        mgx::set_tile32_min_n(value);
+        return MGX_OK;
+    }
+    if (!strcmp(key, "tile_xcd")) {
+        if (value != 0 && value != 1) return fail(MGX_E_ARG, "tile_xcd must be 0 or 1");
+        mgx::set_tile_xcd(value);
+        return MGX_OK;
+    }
+    if (!strcmp(key, "march_order")) {
+        if (value < 0 || value > 3) return fail(MGX_E_ARG, "march_order must be 0..3");
+        mgx::set_march_order(value);
+        return MGX_OK;
+    }
     return fail(MGX_E_ARG, std::string("mgx_set_tuning: unknown key ") + key);
 }
 extern "C" int mgx_get_tuning(const char *key, long *value) {
@@ -962,6 +977,18 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "xfast")) {
         *value = mgx::get_xfast();
+        return MGX_OK;
+    }
+    if (!strcmp(key, "tile32_min_n")) {
+        *value = mgx::get_tile32_min_n();
+        return MGX_OK;
+    }
+    if (!strcmp(key, "tile_xcd")) {
+        *value = mgx::get_tile_xcd();
+        return MGX_OK;
+    }
+    if (!strcmp(key, "march_order")) {
+        *value = mgx::get_march_order();
         return MGX_OK;
     }
     return fail(MGX_E_ARG, std::string("mgx_get_tuning: unknown key ") + key);

@@ -122,3 +122,34 @@ def test_unguarded_interior_kernel_equals_guarded(N, L, G, cross):
         _lib.set_tuning("xfast", old)
     assert np.array_equal(u0_, u1_)
     np.testing.assert_allclose(n1, n0, rtol=NORM_RTOL)
+
+
+@pytest.fixture
+def knobs():
+    """Set tuning keys for one test; restores the previous values."""
+    saved = {}
+
+    def set_(**kv):
+        for k, v in kv.items():
+            saved.setdefault(k, _lib.get_tuning(k))
+            _lib.set_tuning(k, v)
+    yield set_
+    for k, v in saved.items():
+        _lib.set_tuning(k, v)
+
+
+@pytest.mark.parametrize("N,L,G", [(8192, 5, 1), (4096, 6, 4)], ids=["N8192", "N4096_G4"])
+def test_work_order_does_not_change_results(N, L, G, cross, knobs):
+    """march_order (band-major rows, XCD-contiguous workgroups) and tile_xcd /
+    tile32_min_n (tile order and 32-row tiles) only reorder the work: u
+    bitwise, norms to the summation-order tolerance, on one GPU and on row
+    blocks."""
+    cross(1)
+    kw = dict(local_parts=G) if G > 1 else {}
+    knobs(march_order=0, tile_xcd=0, tile32_min_n=1 << 30)
+    u_ref, n_ref = _cycles_plain(N, L, 3, **kw)
+    for mo, tx, t32 in ((1, 0, 1 << 30), (2, 1, 0), (3, 1, 1024)):
+        knobs(march_order=mo, tile_xcd=tx, tile32_min_n=t32)
+        u, n = _cycles_plain(N, L, 3, **kw)
+        assert np.array_equal(u, u_ref), (mo, tx, t32)
+        np.testing.assert_allclose(n, n_ref, rtol=NORM_RTOL)

@@ -101,14 +101,19 @@ def test_context_tower_matches_oracle(oracle_mod, tower_mode):
 SMOOTHERS = [(0, 3), (0, 2), (0, 1), (1, 3), (2, 3)]   # (smoother, sweeps fused per pass)
 
 
-@pytest.fixture(params=[2048, 0], ids=["tile", "march"])
+@pytest.fixture(params=[(2048, 1 << 30, 0), (2048, 0, 1), (0, 1 << 30, 0)],
+                ids=["tile", "tile32xcd", "march"])
 def tile_mode(request):
-    """Small levels as 2-D LDS tiles (default) or as the row march."""
+    """Small levels as 2-D LDS tiles (16-row; or 32-row tiles in XCD order) or
+    as the row march."""
     from hpcclassmultigridproject_amd import _lib
-    old = _lib.get_tuning("tile_max_n")
-    _lib.set_tuning("tile_max_n", request.param)
-    yield request.param
-    _lib.set_tuning("tile_max_n", old)
+    keys = ("tile_max_n", "tile32_min_n", "tile_xcd")
+    old = [_lib.get_tuning(k) for k in keys]
+    for k, v in zip(keys, request.param):
+        _lib.set_tuning(k, v)
+    yield request.param[0]
+    for k, v in zip(keys, old):
+        _lib.set_tuning(k, v)
 
 
 @pytest.mark.parametrize("smoother,fuse", SMOOTHERS)
