@@ -113,13 +113,15 @@ long get_xfast();
 void set_tile_max_n(long v);
 long get_tile_max_n();
 // K = 3 tile passes on levels n >= tile32_min_n use 32 x 64 output tiles
-// (default: off), others 16 x 64; tile_xcd = 1 deals the tiles XCD-contiguous.
+// (default 2048), others 16 x 64; tile_xcd = 1 (default) deals the tiles
+// XCD-contiguous.
 void set_tile32_min_n(long v);
 long get_tile32_min_n();
 void set_tile_xcd(long v);
 long get_tile_xcd();
 // Row-march work order: bit 0 = band-major (neighbouring strip groups march
-// the same rows together), bit 1 = XCD-contiguous workgroup order.
+// the same rows together; launches of >= 192 rows per workgroup), bit 1 =
+// XCD-contiguous workgroup order.  Default 3.
 void set_march_order(long v);
 long get_march_order();
 // Workgroup width (lanes) of the row march on levels with n >= 4096: 128 or 256.
