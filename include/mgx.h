@@ -172,7 +172,14 @@ int mgx_synchronize(mgx_ctx *ctx);
  * would be shorter than this (default 256, even, >= 16); read at creation.
  * "xfast": 1 (default) runs the cross-cycle pass as an unguarded kernel over
  * the interior strips and rows plus a guarded kernel over the boundary strips
- * and bands; 0 = one guarded launch (bitwise the same results). */
+ * and bands; 0 = one guarded launch (bitwise the same results).
+ * "march_order": work order of the row marches, bit 0 = band-major (the
+ * workgroups of neighbouring strip groups march the same rows at the same
+ * time, so their shared halo columns are fetched once; launches with >= 192
+ * rows per workgroup), bit 1 = XCD-contiguous workgroup order; default 3
+ * (env MGX_MARCH_ORDER).  "tile_xcd": 1 (default) deals the LDS tiles
+ * XCD-contiguous.  "tile32_min_n": K=3 tile passes on levels n >= value use
+ * 32-row tiles (default 2048).  None of them changes a result bit. */
 int mgx_set_tuning(const char *key, long value);
 int mgx_get_tuning(const char *key, long *value);
 
