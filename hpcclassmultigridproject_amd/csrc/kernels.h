@@ -124,6 +124,10 @@ long get_tile_xcd();
 // XCD-contiguous workgroup order.  Default 3.
 void set_march_order(long v);
 long get_march_order();
+// Fewest rows per workgroup of a wave-march launch (default 64): fewer,
+// longer segments amortise the warm-up rows, more keep more waves in flight.
+void set_march_min_rows(long v);
+long get_march_min_rows();
 // Workgroup width (lanes) of the row march on levels with n >= 4096: 128 or 256.
 void set_march_block(long v);
 void set_march_kernel(long v);

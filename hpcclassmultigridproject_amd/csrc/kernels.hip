@@ -1856,6 +1856,11 @@ static void march_regions(long n, int W, int H, int ra, int rb, int top, int bot
     }
 }
 
+long g_march_min_rows = 64;   // fewest rows per workgroup of a wave march (tuning key)
+static long march_min_rows() { return g_march_min_rows; }
+void set_march_min_rows(long v) { g_march_min_rows = v; }
+long get_march_min_rows() { return g_march_min_rows; }
+
 long g_march_order = -1;   // tuning key "march_order": bit 0 bands, bit 1 XCD order
 static long march_order() {
     if (g_march_order < 0) {
@@ -1897,7 +1902,7 @@ static int wsmooth_launch(const SmoothArgs &A, const MarchRegions &reg, double *
                                                            64 * WPB, 0);
         slots = std::max(1, cus) * std::max(1, per);
     }
-    long g = std::max<long>(1, std::min<long>(slots, total / 64));
+    long g = std::max<long>(1, std::min<long>(slots, total / march_min_rows()));
     g = std::min<long>(g, max_wgs);
     const long upw = (total + g - 1) / g;
     const unsigned grid = (unsigned)((total + upw - 1) / upw);

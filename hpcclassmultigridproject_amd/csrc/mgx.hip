@@ -950,6 +950,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgx::set_march_order(value);
         return MGX_OK;
     }
+    if (!strcmp(key, "march_min_rows")) {
+        if (value < 8) return fail(MGX_E_ARG, "march_min_rows must be >= 8");
+        mgx::set_march_min_rows(value);
+        return MGX_OK;
+    }
     return fail(MGX_E_ARG, std::string("mgx_set_tuning: unknown key ") + key);
 }
 extern "C" int mgx_get_tuning(const char *key, long *value) {
@@ -989,6 +994,10 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "march_order")) {
         *value = mgx::get_march_order();
+        return MGX_OK;
+    }
+    if (!strcmp(key, "march_min_rows")) {
+        *value = mgx::get_march_min_rows();
         return MGX_OK;
     }
     return fail(MGX_E_ARG, std::string("mgx_get_tuning: unknown key ") + key);
