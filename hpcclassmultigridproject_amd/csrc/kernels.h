@@ -107,6 +107,10 @@ int launch_xsmooth(const XArgs &a, int sweeps, hipStream_t s);
 // Cross pass: 1 = interior strips run the unguarded march (default), 0 = all guarded.
 void set_xfast(long v);
 long get_xfast();
+// Cross pass: 1 = its edge kernel runs on a side stream, overlapping the
+// interior kernel's tail (joined before the next launch on the caller's stream).
+void set_xoverlap(long v);
+long get_xoverlap();
 // Levels with n <= tile_max_n use the 2-D tile form of the fused pass (small
 // levels: latency bound), larger ones the row march.  Default 2048, or the
 // MGX_TILE_MAX_N environment variable.

@@ -1925,6 +1925,31 @@ static int smooth_winst(const SmoothArgs &A, hipStream_t s) {
 }
 
 
+long g_xoverlap = 0;   // tuning key "xoverlap"
+void set_xoverlap(long v) { g_xoverlap = v; }
+long get_xoverlap() { return g_xoverlap; }
+
+// One non-blocking side stream + fork/join events per device (created on first use).
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+static SideStream *side_stream() {
+    static SideStream per_dev[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    SideStream &ss = per_dev[dev];
+    if (!ss.s) {
+        if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess) {
+            ss = SideStream{};
+            return nullptr;
+        }
+    }
+    return &ss;
+}
+
 template <int WPB, int K, bool G>
 static int xsmooth_slots() {
     static int slots = 0;   // resident workgroups of this instantiation
@@ -1984,8 +2009,23 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
     march_regions<1>(n, X::W, X::H, ra, rb, X::TOP, X::BOT, split, unused, edge);
     const int pm = xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, 64,
                                                  kNormBlocks / WPB / 2, s);
+    // xoverlap: the edge kernel on a side stream (forked after the inner
+    // launch, joined before the caller's next launch), so its workgroups take
+    // the CUs the inner kernel's last workgroups free.  Outputs are disjoint
+    // (strips / rows, partials ranges); inputs are read only.
+    hipStream_t se = s;
+    SideStream *ss = g_xoverlap && pm > 0 ? side_stream() : nullptr;
+    if (ss) {
+        (void)hipEventRecord(ss->fork, s);
+        (void)hipStreamWaitEvent(ss->s, ss->fork, 0);
+        se = ss->s;
+    }
     const int pe = xsmooth_launch<1, K, true>(A, edge, A.partials + pm, lo, hi, 32,
-                                              kNormBlocks / 2, s);
+                                              kNormBlocks / 2, se);
+    if (ss) {
+        (void)hipEventRecord(ss->join, ss->s);
+        (void)hipStreamWaitEvent(s, ss->join, 0);
+    }
     return pm + pe;
 }
 

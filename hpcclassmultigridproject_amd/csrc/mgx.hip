@@ -955,6 +955,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgx::set_march_min_rows(value);
         return MGX_OK;
     }
+    if (!strcmp(key, "xoverlap")) {
+        if (value != 0 && value != 1) return fail(MGX_E_ARG, "xoverlap must be 0 or 1");
+        mgx::set_xoverlap(value);
+        return MGX_OK;
+    }
     return fail(MGX_E_ARG, std::string("mgx_set_tuning: unknown key ") + key);
 }
 extern "C" int mgx_get_tuning(const char *key, long *value) {
@@ -998,6 +1003,10 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "march_min_rows")) {
         *value = mgx::get_march_min_rows();
+        return MGX_OK;
+    }
+    if (!strcmp(key, "xoverlap")) {
+        *value = mgx::get_xoverlap();
         return MGX_OK;
     }
     return fail(MGX_E_ARG, std::string("mgx_get_tuning: unknown key ") + key);

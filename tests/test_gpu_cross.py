@@ -140,16 +140,17 @@ def knobs():
 
 @pytest.mark.parametrize("N,L,G", [(8192, 5, 1), (4096, 6, 4)], ids=["N8192", "N4096_G4"])
 def test_work_order_does_not_change_results(N, L, G, cross, knobs):
-    """march_order (band-major rows, XCD-contiguous workgroups) and tile_xcd /
-    tile32_min_n (tile order and 32-row tiles) only reorder the work: u
+    """march_order (band-major rows, XCD-contiguous workgroups), tile_xcd /
+    tile32_min_n (tile order and 32-row tiles) and xoverlap (the cross pass's
+    edge kernel on a side stream) only reorder the work: u
     bitwise, norms to the summation-order tolerance, on one GPU and on row
     blocks."""
     cross(1)
     kw = dict(local_parts=G) if G > 1 else {}
-    knobs(march_order=0, tile_xcd=0, tile32_min_n=1 << 30)
+    knobs(march_order=0, tile_xcd=0, tile32_min_n=1 << 30, xoverlap=0)
     u_ref, n_ref = _cycles_plain(N, L, 3, **kw)
-    for mo, tx, t32 in ((1, 0, 1 << 30), (2, 1, 0), (3, 1, 1024)):
-        knobs(march_order=mo, tile_xcd=tx, tile32_min_n=t32)
+    for mo, tx, t32, xo in ((1, 0, 1 << 30, 0), (2, 1, 0, 1), (3, 1, 1024, 1)):
+        knobs(march_order=mo, tile_xcd=tx, tile32_min_n=t32, xoverlap=xo)
         u, n = _cycles_plain(N, L, 3, **kw)
-        assert np.array_equal(u, u_ref), (mo, tx, t32)
+        assert np.array_equal(u, u_ref), (mo, tx, t32, xo)
         np.testing.assert_allclose(n, n_ref, rtol=NORM_RTOL)
