@@ -179,7 +179,10 @@ int mgx_synchronize(mgx_ctx *ctx);
  * rows per workgroup), bit 1 = XCD-contiguous workgroup order; default 3
  * (env MGX_MARCH_ORDER).  "tile_xcd": 1 (default) deals the LDS tiles
  * XCD-contiguous.  "tile32_min_n": K=3 tile passes on levels n >= value use
- * 32-row tiles (default 2048).  None of them changes a result bit. */
+ * 32-row tiles (default 2048).  "march_min_rows": fewest rows per workgroup
+ * of a wave-march launch (default 64, >= 8).  "xoverlap": 1 runs the cross
+ * pass's edge kernel on a side stream next to the interior kernel (default 0).
+ * None of them changes a result bit. */
 int mgx_set_tuning(const char *key, long value);
 int mgx_get_tuning(const char *key, long *value);
 

@@ -83,3 +83,31 @@ def test_init_problem_rows_are_rows_of_the_full_init():
         sl = slice(r0 * w, r1 * w)
         assert np.array_equal(a, u0[sl]) and np.array_equal(b, v1[sl])
         assert np.array_equal(c, v2[sl])
+
+
+TUNING_KEYS = {   # key -> (a valid value, an invalid value or None)
+    "tile_max_n": (1024, None), "march_block": (128, 100), "cross_cycle": (0, 2),
+    "march_kernel": (0, 3), "dist_min_rows": (64, 7), "xfast": (0, 2),
+    "tile32_min_n": (1024, -1), "tile_xcd": (0, 2), "march_order": (1, 4),
+    "march_min_rows": (96, 4), "xoverlap": (1, 2),
+}
+
+
+def test_tuning_keys_documented_round_trip_and_validate():
+    """Every key mgx.h documents is accepted, reads back what was set, refuses
+    out-of-range values with a status, and unknown keys are errors."""
+    hdr = open(_lib.HEADER_PATH).read()
+    for key, (good, bad) in TUNING_KEYS.items():
+        assert f'"{key}"' in hdr, f"{key} not documented in mgx.h"
+        old = _lib.get_tuning(key)
+        try:
+            _lib.set_tuning(key, good)
+            assert _lib.get_tuning(key) == good
+            if bad is not None:
+                with pytest.raises(_lib.MGXError):
+                    _lib.set_tuning(key, bad)
+                assert _lib.get_tuning(key) == good
+        finally:
+            _lib.set_tuning(key, old)
+    with pytest.raises(_lib.MGXError):
+        _lib.set_tuning("no_such_key", 1)
