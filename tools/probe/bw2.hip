@@ -195,6 +195,50 @@ __global__ __launch_bounds__(256) void k_dmarch(const double2 *__restrict__ a,
     }
 }
 
+
+// flat, but workgroup b streams block perm(b): a fixed odd-multiplier
+// permutation of the 4-KiB blocks (scatters the chip's active window)
+template <bool NT>
+__global__ __launch_bounds__(256) void k_flatperm(const double2 *__restrict__ a,
+                                                  const double2 *__restrict__ b,
+                                                  const double2 *__restrict__ c,
+                                                  const double2 *__restrict__ d,
+                                                  double2 *__restrict__ o, long n, long nb,
+                                                  long mult) {
+    const long blk = ((long)blockIdx.x * mult) % nb;
+    const long i = blk * 256 + threadIdx.x;
+    if (i >= n) return;
+    double2 v = ld<NT>(a + i);
+    const double2 y = ld<NT>(b + i), z = ld<NT>(c + i), w = ld<NT>(d + i);
+    v.x += y.x + z.x + w.x;
+    v.y += y.y + z.y + w.y;
+    st<NT>(o + i, v);
+}
+// flat over a strip-interleaved order: workgroup b -> row (b % rows), strip
+// (b / rows): consecutive workgroups walk DOWN a column strip (a march's
+// address order, but every row piece its own workgroup)
+template <bool NT>
+__global__ __launch_bounds__(64) void k_flatcol(const double2 *__restrict__ a,
+                                                const double2 *__restrict__ b,
+                                                const double2 *__restrict__ c,
+                                                const double2 *__restrict__ d,
+                                                double2 *__restrict__ o, long pitch2, int rows,
+                                                int strips, int seg) {
+    // seg rows per strip visit: b -> (strip, row) with rows grouped in segments
+    const long bb = blockIdx.x;
+    const long per = (long)seg * strips;
+    const int band = (int)(bb / per);
+    const long rem = bb % per;
+    const int strip = (int)(rem / seg), row = band * seg + (int)(rem % seg);
+    if (row >= rows) return;
+    const long i = (long)row * pitch2 + (long)strip * 64 + threadIdx.x;
+    double2 v = ld<NT>(a + i);
+    const double2 y = ld<NT>(b + i), z = ld<NT>(c + i), w = ld<NT>(d + i);
+    v.x += y.x + z.x + w.x;
+    v.y += y.y + z.y + w.y;
+    st<NT>(o + i, v);
+}
+
 static hipEvent_t e0, e1;
 template <typename F>
 static double timeit(F go, double bytes) {
@@ -292,6 +336,22 @@ int main() {
             printf("dmarch P=4 nt R=%d waves/CU=%d: %.0f GB/s\n", R, wpc, timeit([&] {
                        hipMemsetAsync(ctr, 0, 4);
                        k_dmarch<4, true><<<g, 256>>>(A, B, Cc, D, O, pitch2, rows, strips, R, ctr);
+                   }, mbytes));
+        }
+    }
+
+    {
+        const long nb = (n + 255) / 256;
+        for (long mult : {1L, 7919L, 1000003L}) {
+            printf("flatperm mult=%ld: %.0f GB/s\n", mult, timeit([&] {
+                       k_flatperm<false><<<(unsigned)nb, 256>>>(A, B, Cc, D, O, n, nb, mult);
+                   }, 5.0 * bytes));
+        }
+        for (int seg : {1, 8, 64, 1024}) {
+            const long nblk = (long)strips * rows;
+            printf("flatcol seg=%d: %.0f GB/s\n", seg, timeit([&] {
+                       k_flatcol<false><<<(unsigned)nblk, 64>>>(A, B, Cc, D, O, pitch2, rows,
+                                                               strips, seg);
                    }, mbytes));
         }
     }
