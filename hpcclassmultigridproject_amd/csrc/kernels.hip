@@ -831,7 +831,11 @@ __device__ __forceinline__ double res_point_t(double rhs, double t1, double t2, 
 // G = false: the unguarded march (interior strips, rows [TOP, n+1-BOT) of
 // WCfg: no per-stage predicates), G = true: guarded (see k_xsmooth).
 template <int WPB, int K, int MODE, bool G>
+#ifdef MGX_WS_WAVES   // experiment: minimum waves per SIMD for the wave march
+__global__ __launch_bounds__(64 * WPB, MGX_WS_WAVES) void k_wsmooth(
+#else
 __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
+#endif
     const double *__restrict__ uin, double *__restrict__ uout, const double *__restrict__ rhs,
     const double *__restrict__ v1, const double *__restrict__ v2, const double *__restrict__ uc,
     long pitchc, double *__restrict__ rhsc, double *__restrict__ partials, int n, long pitch,
