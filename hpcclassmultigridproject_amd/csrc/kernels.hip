@@ -78,12 +78,6 @@ __device__ __forceinline__ void st2(double *p, double2 v) {
 // Streaming (non-temporal) forms for data touched once per pass: the fused
 // smoother's rhs/v1/v2/u rows and its output rows.  MGX_NT=0 turns them into
 // plain accesses (A/B builds).
-#ifndef MGX_WSYNC
-#define MGX_WSYNC 0
-#endif
-#ifndef MGX_XPRIO
-#define MGX_XPRIO 0   // experiment: s_setprio 1 for the B (1) / A (2) waves of k_xsmooth
-#endif
 #ifndef MGX_NT
 #define MGX_NT 1
 #endif
@@ -831,11 +825,7 @@ __device__ __forceinline__ double res_point_t(double rhs, double t1, double t2, 
 // G = false: the unguarded march (interior strips, rows [TOP, n+1-BOT) of
 // WCfg: no per-stage predicates), G = true: guarded (see k_xsmooth).
 template <int WPB, int K, int MODE, bool G>
-#ifdef MGX_WS_WAVES   // experiment: minimum waves per SIMD for the wave march
-__global__ __launch_bounds__(64 * WPB, MGX_WS_WAVES) void k_wsmooth(
-#else
 __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
-#endif
     const double *__restrict__ uin, double *__restrict__ uout, const double *__restrict__ rhs,
     const double *__restrict__ v1, const double *__restrict__ v2, const double *__restrict__ uc,
     long pitchc, double *__restrict__ rhsc, double *__restrict__ partials, int n, long pitch,
@@ -1030,11 +1020,6 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                 }
                 // (5) rhs/v row s+3 into the slot of row s+3-NR (dead)
                 load_rv(s + 3, rd[(p + 3) % NR]);
-#if MGX_WSYNC
-                // experiment: keep the WPB waves in step so the halo columns
-                // a neighbour loads are still in L2
-                if (MGX_WSYNC == 1 || (p & 1)) __builtin_amdgcn_s_barrier();
-#endif
                 if (++s > s_last) goto done;
             }
         }
@@ -1107,11 +1092,6 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     const int wv = threadIdx.x >> 6;
     const bool isA = wv < WPB;   // wave-uniform role
     const int pr = isA ? wv : wv - WPB;
-#if MGX_XPRIO == 1
-    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 64 * WPB) __builtin_amdgcn_s_setprio(1);
-#elif MGX_XPRIO == 2
-    if (__builtin_amdgcn_readfirstlane(threadIdx.x) < 64 * WPB) __builtin_amdgcn_s_setprio(1);
-#endif
     const long total = reg.pre[reg.count];
     long start = wg_order(reg) * units_per_wg;
     const long end = min(total, start + units_per_wg);
