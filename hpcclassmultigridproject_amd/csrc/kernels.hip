@@ -1415,6 +1415,28 @@ __global__ __launch_bounds__(256) void k_smooth_tile(
         }
         st2(&tu[r * WT + 2 * k], v);
     }
+    // per pair, once: its LDS index, row parity and which of its two points
+    // the stages may update (interior of the level and of the extended tile);
+    // the stage loop then does no index arithmetic
+    int xs[PPT];
+    unsigned upd = 0, rpar = 0;   // bits 2m / 2m+1: column 2k / 2k+1 updatable; bit m: row odd
+#pragma unroll
+    for (int m = 0; m < PPT; ++m) {
+        const int q = t + m * 256;
+        xs[m] = 0;
+        if (q >= T::PAIRS || !ok[m]) continue;
+        const int r = q / HW, k = q % HW;
+        const long gi = i0 + r;
+        xs[m] = r * WT + 2 * k;
+        rpar |= (unsigned)(r & 1) << m;
+#pragma unroll
+        for (int cs = 0; cs < 2; ++cs) {
+            const long gj = j0 + 2 * k + cs;
+            if (gi >= 1 && gi <= n - 1 && gj >= 1 && gj <= n - 1 && r >= 1 && r <= T::RT - 2 &&
+                2 * k + cs >= 1 && 2 * k + cs <= WT - 2)
+                upd |= 1u << (2 * m + cs);
+        }
+    }
     __syncthreads();
 
 #pragma unroll
@@ -1422,14 +1444,10 @@ __global__ __launch_bounds__(256) void k_smooth_tile(
 #pragma unroll
         for (int m = 0; m < PPT; ++m) {
             const int q = t + m * 256;
-            if (q >= T::PAIRS || !ok[m]) continue;
-            const int r = q / HW, k = q % HW;
-            const long gi = i0 + r;
-            const int cs = (r & 1) ^ (h & 1);   // origin parity is even
-            const long gj = j0 + 2 * k + cs;
-            if (gi < 1 || gi > n - 1 || gj < 1 || gj > n - 1) continue;
-            if (r < 1 || r > T::RT - 2 || (2 * k + cs) < 1 || (2 * k + cs) > WT - 2) continue;
-            const int x = r * WT + 2 * k + cs;
+            if (q >= T::PAIRS) continue;
+            const int cs = (int)((rpar >> m) & 1u) ^ (h & 1);   // origin parity is even
+            if (!((upd >> (2 * m + cs)) & 1u)) continue;
+            const int x = xs[m] + cs;
             const double fr = cs ? f1[m] : f0[m], fx = cs ? x1[m] : x0[m],
                          fy = cs ? y1[m] : y0[m];
             tu[x] = gs_point_fast(fr, fx, fy, tu[x - WT], tu[x - 1], tu[x + WT], tu[x + 1], c);
