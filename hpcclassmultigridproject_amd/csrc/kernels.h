@@ -168,5 +168,8 @@ void launch_coarse_solve(double *u, const double *rhs, const double *v1, const d
                          long n, long pitch, Coef c, double tol, int maxit, bool zero_first,
                          double *stats, hipStream_t s);
 constexpr long kCoarseOneWgMaxN = 256;
+// 1 (default): coarsest levels n <= 64 solve with u, rhs, v1, v2 in LDS.
+void set_coarse_lds(long v);
+long get_coarse_lds();
 
 }  // namespace mgx

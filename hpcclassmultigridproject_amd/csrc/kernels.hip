@@ -1699,6 +1699,73 @@ __global__ __launch_bounds__(1024) void k_coarse_solve(double *u, const double *
     }
 }
 
+// The same solve with u, rhs, v1, v2 held in LDS (n <= 64: 4 x 65^2 doubles
+// = 135 KB of the CU's 160 KB): the loop's loads and stores are LDS accesses
+// instead of L2 round trips.  Same sweep order, term order and reduction
+// order as k_coarse_solve, so u, the norms and the iteration count are
+// bitwise those of k_coarse_solve.
+constexpr int kCoarseLdsMaxN = 64;
+__global__ __launch_bounds__(1024) void k_coarse_solve_lds(double *u, const double *rhs,
+                                                           const double *v1, const double *v2,
+                                                           int n, long pitch, Coef c, double tol,
+                                                           int maxit, int zero_first,
+                                                           double *stats) {
+    constexpr int NP = kCoarseLdsMaxN + 1;
+    constexpr int SZ = NP * NP;
+    __shared__ double su[SZ], sr[SZ], sx[SZ], sy[SZ];
+    __shared__ double lds[16];
+    __shared__ double s_norm;
+    const int t = threadIdx.x;
+    const int tx = t & 63, ty = t >> 6;
+    if (zero_first)
+        for (long p = t; p < (long)(n + 1) * pitch; p += 1024) u[p] = 0.0;
+    for (int i = ty; i <= n; i += 16)
+        for (int j = tx; j <= n; j += 64) {
+            const long p = (long)i * pitch + j;
+            const int q = i * NP + j;
+            su[q] = zero_first ? 0.0 : u[p];
+            sr[q] = rhs[p];
+            sx[q] = v1[p];
+            sy[q] = v2[p];
+        }
+    __syncthreads();
+    int it = 0;
+    double res = 1.0;
+    while (it < maxit && res > tol) {
+        for (int colour = 0; colour < 2; ++colour) {
+            for (int i = 1 + ty; i <= n - 1; i += 16) {
+                const int jc = 1 + ((i + 1 + colour) & 1);
+                for (int j = jc + 2 * tx; j <= n - 1; j += 128) {
+                    const int q = i * NP + j;
+                    su[q] = gs_point(sr[q], sx[q], sy[q], su[q - NP], su[q - 1], su[q + NP],
+                                     su[q + 1], c);
+                }
+            }
+            __syncthreads();
+        }
+        double acc = 0.0;
+        for (int i = 1 + ty; i <= n - 1; i += 16)
+            for (int j = 1 + tx; j <= n - 1; j += 64) {
+                const int q = i * NP + j;
+                const double r = res_point(sr[q], sx[q], sy[q], su[q], su[q - NP], su[q - 1],
+                                           su[q + NP], su[q + 1], c);
+                acc += r * r;
+            }
+        double s = block_sum(acc, lds);
+        if (t == 0) s_norm = sqrt(s);
+        __syncthreads();
+        res = s_norm;
+        ++it;
+        __syncthreads();
+    }
+    for (int i = 1 + ty; i <= n - 1; i += 16)
+        for (int j = 1 + tx; j <= n - 1; j += 64) u[(long)i * pitch + j] = su[i * NP + j];
+    if (t == 0) {
+        stats[0] += it;
+        stats[1] = res;
+    }
+}
+
 inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }
 
 }  // namespace
@@ -2291,9 +2358,18 @@ void launch_prolong_add(double *uf, long pitchf, const double *uc, long pitchc, 
     MGX_LAUNCH(k_prolong_add, g, dim3(256), s, uf, pitchf, uc, pitchc, (int)nc);
 }
 
+long g_coarse_lds = 1;   // tuning key "coarse_lds"
+void set_coarse_lds(long v) { g_coarse_lds = v; }
+long get_coarse_lds() { return g_coarse_lds; }
+
 void launch_coarse_solve(double *u, const double *rhs, const double *v1, const double *v2,
                          long n, long pitch, Coef c, double tol, int maxit, bool zero_first,
                          double *stats, hipStream_t s) {
+    if (n <= kCoarseLdsMaxN && g_coarse_lds) {
+        MGX_LAUNCH(k_coarse_solve_lds, dim3(1), dim3(1024), s, u, rhs, v1, v2, (int)n, pitch, c,
+                   tol, maxit, zero_first ? 1 : 0, stats);
+        return;
+    }
     MGX_LAUNCH(k_coarse_solve, dim3(1), dim3(1024), s, u, rhs, v1, v2, (int)n, pitch, c, tol,
                maxit, zero_first ? 1 : 0, stats);
 }

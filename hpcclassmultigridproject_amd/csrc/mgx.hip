@@ -960,6 +960,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgx::set_xoverlap(value);
         return MGX_OK;
     }
+    if (!strcmp(key, "coarse_lds")) {
+        if (value != 0 && value != 1) return fail(MGX_E_ARG, "coarse_lds must be 0 or 1");
+        mgx::set_coarse_lds(value);
+        return MGX_OK;
+    }
     return fail(MGX_E_ARG, std::string("mgx_set_tuning: unknown key ") + key);
 }
 extern "C" int mgx_get_tuning(const char *key, long *value) {
@@ -1007,6 +1012,10 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "xoverlap")) {
         *value = mgx::get_xoverlap();
+        return MGX_OK;
+    }
+    if (!strcmp(key, "coarse_lds")) {
+        *value = mgx::get_coarse_lds();
         return MGX_OK;
     }
     return fail(MGX_E_ARG, std::string("mgx_get_tuning: unknown key ") + key);

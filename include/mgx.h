@@ -182,6 +182,8 @@ int mgx_synchronize(mgx_ctx *ctx);
  * 32-row tiles (default 2048).  "march_min_rows": fewest rows per workgroup
  * of a wave-march launch (default 64, >= 8).  "xoverlap": 1 runs the cross
  * pass's edge kernel on a side stream next to the interior kernel (default 0).
+ * "coarse_lds": 1 (default) solves coarsest levels n <= 64 with the fields
+ * in LDS, 0 = through L2 (bitwise the same).
  * None of them changes a result bit. */
 int mgx_set_tuning(const char *key, long value);
 int mgx_get_tuning(const char *key, long *value);

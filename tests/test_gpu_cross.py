@@ -154,3 +154,19 @@ def test_work_order_does_not_change_results(N, L, G, cross, knobs):
         u, n = _cycles_plain(N, L, 3, **kw)
         assert np.array_equal(u, u_ref), (mo, tx, t32, xo)
         np.testing.assert_allclose(n, n_ref, rtol=NORM_RTOL)
+
+
+@pytest.mark.parametrize("N,L", [(4096, 7), (1024, 6), (256, 4)], ids=["c64", "c32", "c32s"])
+def test_coarse_solve_in_lds_equals_l2_version(N, L, knobs):
+    """coarse_lds: the coarsest solve with its fields in LDS gives bitwise the
+    u, norms and coarse iteration counts of the L2 version."""
+    out = []
+    u0, v1, v2 = init_problem(N)
+    for v in (0, 1):
+        knobs(coarse_lds=v)
+        with Multigrid(N, L, 1.0 / N / 10, NU) as mg:
+            mg.upload(u0, v1, v2)
+            cyc = [mg.step(1e-6) for _ in range(2)]
+            out.append((mg.download(), cyc, mg.coarse_iterations(), mg.residual_norm(0)))
+    (ua, ca, ia, ra), (ub, cb, ib, rb) = out
+    assert np.array_equal(ua, ub) and ca == cb and ia == ib and ra == rb
