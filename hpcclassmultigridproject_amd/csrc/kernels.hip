@@ -1360,7 +1360,13 @@ __global__ __launch_bounds__(256) void k_smooth_tile(
     using C = SmoothCfg<K, MODE>;
     using T = TileCfg<K, MODE, TRV>;
     constexpr int S = C::S, EH = T::EH, WT = T::WT, PPT = T::PPT, HW = WT / 2;
+    // u of the extended tile split by colour: point (r, col) lives in plane
+    // (r + col) & 1 (the tile origin has even parity) at index r*HW + col/2, so
+    // a stage's own points and all four neighbours are consecutive 8-B words
+    // across consecutive lanes (no LDS bank conflicts; interleaved, the
+    // stride-2 accesses were 2-way conflicts on every read)
     __shared__ __attribute__((aligned(16))) double tu[T::RT * WT];
+    constexpr int PL = T::PAIRS;   // plane size = RT * WT / 2
 
     const int t = threadIdx.x;
     int bid = blockIdx.x;
@@ -1413,7 +1419,8 @@ __global__ __launch_bounds__(256) void k_smooth_tile(
             y0[m] = yy.x;
             y1[m] = yy.y;
         }
-        st2(&tu[r * WT + 2 * k], v);
+        tu[(r & 1) * PL + q] = v.x;   // q = r*HW + k
+        tu[((r & 1) ^ 1) * PL + q] = v.y;
     }
     // per pair, once: its LDS index, row parity and which of its two points
     // the stages may update (interior of the level and of the extended tile);
@@ -1427,7 +1434,7 @@ __global__ __launch_bounds__(256) void k_smooth_tile(
         if (q >= T::PAIRS || !ok[m]) continue;
         const int r = q / HW, k = q % HW;
         const long gi = i0 + r;
-        xs[m] = r * WT + 2 * k;
+        xs[m] = q;   // r*HW + k
         rpar |= (unsigned)(r & 1) << m;
 #pragma unroll
         for (int cs = 0; cs < 2; ++cs) {
@@ -1447,10 +1454,13 @@ __global__ __launch_bounds__(256) void k_smooth_tile(
             if (q >= T::PAIRS) continue;
             const int cs = (int)((rpar >> m) & 1u) ^ (h & 1);   // origin parity is even
             if (!((upd >> (2 * m + cs)) & 1u)) continue;
-            const int x = xs[m] + cs;
+            const int b = xs[m];
+            double *own = tu + (h & 1) * PL;           // colour being updated
+            const double *oth = tu + ((h & 1) ^ 1) * PL;   // its neighbours
             const double fr = cs ? f1[m] : f0[m], fx = cs ? x1[m] : x0[m],
                          fy = cs ? y1[m] : y0[m];
-            tu[x] = gs_point_fast(fr, fx, fy, tu[x - WT], tu[x - 1], tu[x + WT], tu[x + 1], c);
+            own[b] = gs_point_fast(fr, fx, fy, oth[b - HW], oth[b - 1 + cs], oth[b + HW],
+                                   oth[b + cs], c);
         }
         __syncthreads();
     }
@@ -1464,25 +1474,26 @@ __global__ __launch_bounds__(256) void k_smooth_tile(
         if (r < EH || r >= EH + T::TR || 2 * k < EH || 2 * k >= EH + T::TC) continue;
         const long gi = i0 + r, gj = j0 + 2 * k;
         if (gi >= rb) continue;
-        const int x = r * WT + 2 * k;
-        st2(uout + gi * pitch + gj, ld2(&tu[x]));
+        const double *p0 = tu + (r & 1) * PL, *p1 = tu + ((r & 1) ^ 1) * PL;
+        const int b = q;   // r*HW + k; column 2k in p0, 2k+1 in p1
+        st2(uout + gi * pitch + gj, make_double2(p0[b], p1[b]));
         if (C::REST || C::NORM) {
             const bool in0 = gi >= 1 && gi <= n - 1 && gj >= 1 && gj <= n - 1;
             const bool in1 = gi >= 1 && gi <= n - 1 && gj + 1 <= n - 1;
             if (C::REST) {
                 if (!(gi & 1) && in0 && gi <= n - 2 && gj <= n - 2)
                     rhsc[(gi >> 1) * pitchc + (gj >> 1)] =
-                        res_point(f0[m], x0[m], y0[m], tu[x], tu[x - WT], tu[x - 1], tu[x + WT],
-                                  tu[x + 1], c);
+                        res_point(f0[m], x0[m], y0[m], p0[b], p1[b - HW], p1[b - 1], p1[b + HW],
+                                  p1[b], c);
             } else {
                 if (in0) {
-                    const double res = res_point(f0[m], x0[m], y0[m], tu[x], tu[x - WT],
-                                                 tu[x - 1], tu[x + WT], tu[x + 1], c);
+                    const double res = res_point(f0[m], x0[m], y0[m], p0[b], p1[b - HW],
+                                                 p1[b - 1], p1[b + HW], p1[b], c);
                     acc += res * res;
                 }
                 if (in1) {
-                    const double res = res_point(f1[m], x1[m], y1[m], tu[x + 1], tu[x + 1 - WT],
-                                                 tu[x], tu[x + 1 + WT], tu[x + 2], c);
+                    const double res = res_point(f1[m], x1[m], y1[m], p1[b], p0[b - HW],
+                                                 p0[b], p0[b + HW], p0[b + 1], c);
                     acc += res * res;
                 }
             }
