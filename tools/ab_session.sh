@@ -4,8 +4,10 @@ set -e
 O=gpurun_out/ab; mkdir -p $O
 T="timeout -k 10"
 $T 300 python3 tools/ab_levels.py march_order=0,1,2,3 tile32_min_n=1073741824,2048,1024 tile_xcd=0,1 --rounds 3 > $O/knobs.log 2>&1
-for v in default xprio1 xprio2; do
-  if [ $v = default ]; then lib=hpcclassmultigridproject_amd/libmgx.so; else lib=hpcclassmultigridproject_amd/libmgx_$v.so; fi
+# variant builds (tools/build_variant.sh NAME -D...) are compared the same way:
+for lib in hpcclassmultigridproject_amd/libmgx.so hpcclassmultigridproject_amd/libmgx_*.so; do
+  [ -f "$lib" ] || continue
+  v=$(basename $lib .so)
   MGX_LIB=$lib $T 200 python3 tools/ab_levels.py march_order=0,3 --rounds 5 > $O/lib_$v.log 2>&1
 done
 for pad in 0 32 48 512; do
