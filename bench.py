@@ -239,8 +239,10 @@ def main():
         per_launch_bytes = b0 / n0
         avg_s = ms0 * 1e-3 / n0
         achieved = per_launch_bytes / avg_s / 1e9
-        kname = KERNEL_IDS.get((kind, lvl)) if (N, L, args.nsmooth, args.smoother,
-                                                args.fuse) == (16384, 9, 3, 0, 3) else None
+        # the committed PMC traffic is per launch of the single-GPU pass; a
+        # rank's row block moves a fraction of it, so it is not reused there
+        kname = KERNEL_IDS.get((kind, lvl)) if (N, L, args.nsmooth, args.smoother, args.fuse,
+                                                world) == (16384, 9, 3, 0, 3, 1) else None
         traffic = None
         if kname:
             kname, traffic = lookup_traffic(kname)
