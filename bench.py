@@ -19,15 +19,21 @@ points per GPU stay within 2x of the 1-GPU run, "scaling": "weak"
 (configs[4], N=65536 on 8 GPUs: --N 65536 --levels 11; above N=16384 each
 rank initialises and uploads only its own rows, with the correct velocity
 tower, so no host or GPU ever holds the whole grid).
-roofline: the dominant kernel (largest device time: a finest-level fused
-smoothing pass) with achieved = its algorithmic bytes per launch (SURVEY 8d:
-40 B/point per RB sweep x 3 sweeps + the fused residual/restriction or
-prolongation/norm work) / its mean duration (HIP events on the context stream,
-inside the timed region); traffic = its measured HBM bytes per launch
-(rocprofv3 PMC, profiles/r1_hbm_traffic.json).
+roofline: the dominant kernel (largest device time: the finest level's fused
+cross-cycle pass) with achieved = its COMPULSORY bytes per launch (every array
+the pass must read or write, once: u, rhs, v1, v2 and the coarse u read, u_pre
+(+ u_post on the cycle whose solution is kept) and the coarse rhs written;
+DESIGN.md section 5) / its mean duration (HIP events on the context stream,
+inside the timed region); frac = achieved / 8 TB/s.  The SURVEY 8d per-op
+canonical bytes the same launch replaces (12 reference ops per HBM pass) are
+reported beside it as canonical_equiv_GBs, never as the fraction.
+traffic = its measured HBM bytes per launch (rocprofv3 PMC, the
+profiles/*_hbm_traffic.json whose kernels.hip hash matches the built source;
+null with a reason when none does).
 cpu_baseline: rank 0, N=1 only: the reference's own mg_inner (oracle/_ref,
-built from the unmodified sources with the reference Makefile flags), one
-V-cycle of the same workload, OpenMP tasks on the host cores.
+built from the unmodified sources), OpenMP tasks: the reference Makefile's
+-O0 build and an -O3 build, each serial and on all host cores this process may
+use (sched affinity, capped by the cgroup CPU quota); value = the fastest.
 """
 from __future__ import annotations
 
@@ -48,15 +54,35 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s HBM3E
 KERNEL_IDS = {(8, 0): ("mgx::k_xsmooth<4, 3, false>", "mgx::k_xsmooth<1, 3, true>"),
               (0, 0): ("mgx::k_wsmooth<4, 3, 4, true>",),
               (7, 0): ("mgx::k_wsmooth<4, 3, 10, true>",)}
-TRAFFIC_JSON = os.path.join(ROOT, "profiles", "r1_hbm_traffic.json")
+KERNELS_HIP = os.path.join(ROOT, "hpcclassmultigridproject_amd", "csrc", "kernels.hip")
+
+
+def kernels_sha():
+    import hashlib
+    return hashlib.sha256(open(KERNELS_HIP, "rb").read()).hexdigest()
+
+
+def traffic_profile():
+    """(path, kernels) of the newest profiles/*_hbm_traffic.json collected from
+    the kernels.hip that is built now, or (None, reason)."""
+    import glob
+    sha = kernels_sha()
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hbm_traffic.json")),
+                   key=os.path.getmtime, reverse=True)
+    for f in files:
+        d = json.load(open(f))
+        if d.get("kernels_hip_sha256") == sha:
+            return os.path.relpath(f, ROOT), d["kernels"]
+    return None, (f"no profiles/*_hbm_traffic.json matches kernels.hip sha256 {sha[:12]} "
+                  "(regenerate with tools/profile_round.sh)")
 
 
 def lookup_traffic(knames):
     """HBM bytes per dispatch of the finest-level instances (largest traffic) of
     the kernels in knames, summed (one launch of the op = one dispatch of each)."""
-    if not os.path.exists(TRAFFIC_JSON):
-        return None, None
-    kernels = json.load(open(TRAFFIC_JSON))["kernels"]
+    path, kernels = traffic_profile()
+    if path is None:
+        return None, None, kernels
     keys, total = [], 0.0
     for kname in knames:
         best = None
@@ -64,10 +90,10 @@ def lookup_traffic(knames):
             if key.split(" grid=")[0] == kname and (best is None or v["hbm_bytes"] > best[1]):
                 best = (key, v["hbm_bytes"])
         if best is None:
-            return None, None
+            return None, None, f"{kname} not in {path}"
         keys.append(best[0])
         total += best[1]
-    return " + ".join(keys), total
+    return " + ".join(keys), total, path
 
 
 def parse():
@@ -83,7 +109,9 @@ def parse():
     ap.add_argument("--fuse", type=int, default=3, help="smoother 0: sweeps per HBM pass")
     ap.add_argument("--cpu-baseline", choices=["auto", "off", "reference", "port"],
                     default="auto")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the all-cores CPU legs (0: every host CPU this "
+                         "process may use)")
     ap.add_argument("--weak", action="store_true",
                     help="multi-GPU: grow N with the GPU count (N*2 per 4x GPUs) instead of "
                          "partitioning the same grid")
@@ -94,19 +122,58 @@ def parse():
     return ap.parse_args()
 
 
+def host_cpus():
+    """CPUs this process may use (affinity, capped by the cgroup v2 quota) and
+    what the host reports."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(quota)))
+    return {"usable": usable, "affinity": aff, "nproc_host": os.cpu_count(),
+            "cgroup_quota_cpus": quota, "model": model,
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
+
+
 def cpu_baseline(args):
-    """Reference V-cycle on the host (bounded sample: one V-cycle)."""
+    """The reference's own mg_inner on the host: -O0 (reference Makefile) and
+    -O3 builds, serial and all usable cores.  Bounded sample: one V-cycle each;
+    the serial legs at N/2 (a quarter of the work, same per-unknown loops) so
+    the whole baseline stays ~30 s."""
     from oracle import oracle as O
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    cpus = host_cpus()
+    allc = args.cpu_threads or cpus["usable"]
     N, L, nu = args.N, args.levels, -4e-4
     kind = args.cpu_baseline
     if kind == "auto":
         kind = "reference" if O.ref_available() else "port"
+    runs = []
     if kind == "reference":
-        secs, setup, res = O.ref_time_vcycles(N, L, nu, 1, threads)
-        build = "reference gs.cpp+multigrid.cpp, -O0 -fopenmp (reference Makefile flags), OMP tasks"
+        legs = [("O3", allc, N, L), ("O0", allc, N, L), ("O3", 1, N // 2, L - 1),
+                ("O0", 1, N // 2, L - 1)]
+        for opt, th, n, lv in legs:
+            if opt == "O3" and not O.ref_o3_available():
+                continue
+            secs, setup, res = O.ref_time_vcycles(n, lv, nu, 1, th, opt=opt)
+            runs.append({"build": opt, "threads": th, "N": n, "levels": lv,
+                         "seconds_per_vcycle": round(secs, 4),
+                         "value": (n - 1) ** 2 / secs})
+        flags = {"O0": "-O0 -fopenmp (reference Makefile flags)",
+                 "O3": "-O3 -march=x86-64-v3 -fopenmp"}
     else:
-        O.set_threads(threads)
+        O.set_threads(allc)
         u0, v1, v2 = O.init_problem(N)
         dt = 1.0 / N / 10
         t = O.Tower(u0, v1, v2, N, L)
@@ -118,11 +185,17 @@ def cpu_baseline(args):
         O.residual(t.ufine, t.rhsfine, N, t.level("v1", 0), t.level("v2", 0), dt, nu, 1.0 / N,
                    res=t.tmp)
         secs = time.perf_counter() - t0
-        build = "oracle/mg_oracle.c restatement, gcc -O2 -fopenmp, OMP parallel-for rows"
-    return {"value": (N - 1) ** 2 / secs, "unit": "grid-point-updates/s", "cores": threads,
-            "kind": kind, "seconds_per_vcycle": secs,
-            "sample": f"1 V-cycle (mg_inner + residual + norm) at N={N}, L={L}, nu_smooth=3, "
-                      f"{threads} host threads; {build}"}
+        runs.append({"build": "port -O2", "threads": allc, "N": N, "levels": L,
+                     "seconds_per_vcycle": round(secs, 4), "value": (N - 1) ** 2 / secs})
+        flags = {"port -O2": "oracle/mg_oracle.c restatement, gcc -O2 -fopenmp"}
+    best = max((r for r in runs if r["N"] == N), key=lambda r: r["value"])
+    return {"value": best["value"], "unit": "grid-point-updates/s", "cores": best["threads"],
+            "kind": kind, "build": flags[best["build"]],
+            "seconds_per_vcycle": best["seconds_per_vcycle"], "runs": runs, "host": cpus,
+            "sample": f"1 V-cycle (mg_inner + residual + norm) per leg, OpenMP tasks of the "
+                      f"reference; all-core legs at N={N}, L={L}, nu_smooth=3 on "
+                      f"{allc} threads; serial legs at N={N // 2}, L={L - 1} (per-unknown "
+                      f"rate); value = the fastest leg at N={N}"}
 
 
 def main():
@@ -204,9 +277,9 @@ def main():
     # in the timed region
     best = None
     for kind in _lib.KERNEL_NAMES:
-        n, ms, b = mg.profile_get(kind, 0)
+        n, ms, b, cb = mg.profile_get_ex(kind, 0)
         if n and (best is None or ms > best[3]):
-            best = (kind, 0, n, ms, b)
+            best = (kind, 0, n, ms, b, cb)
     mg.profile(False)
 
     # per-kernel, per-level breakdown: a few more cycles, every launch timed
@@ -218,11 +291,14 @@ def main():
         mg.profile(True)
         mg.run_cycles(prof_steps)
         for kind, name in _lib.KERNEL_NAMES.items():
-            n, ms, b = mg.profile_get(kind, -1)
+            n, ms, b, cb = mg.profile_get_ex(kind, -1)
             if n:
                 kernels[name] = {"launches_per_step": n / prof_steps,
                                  "ms_per_step": round(ms / prof_steps, 4),
-                                 "algo_GBs": round(b / (ms * 1e-3) / 1e9, 1) if ms > 0 else None}
+                                 "compulsory_GBs": round(cb / (ms * 1e-3) / 1e9, 1)
+                                 if ms > 0 else None,
+                                 "canonical_equiv_GBs": round(b / (ms * 1e-3) / 1e9, 1)
+                                 if ms > 0 else None}
                 for lvl in range(L):
                     nl, msl, bl = mg.profile_get(kind, lvl)
                     if nl:
@@ -232,29 +308,36 @@ def main():
 
     roof = None
     if best:
-        kind, lvl, n0, ms0, b0 = best
-        # algorithmic bytes per launch: 40 B/point per RB sweep,
-        # x the sweeps one launch performs, + the fused residual/restriction,
-        # prolongation+add or residual+norm it absorbs
-        per_launch_bytes = b0 / n0
+        kind, lvl, n0, ms0, b0, cb0 = best
+        # achieved = compulsory bytes per launch (each array the fused pass must
+        # read or write, once) / live mean duration; the per-op canonical bytes
+        #  of the reference ops it replaces go in canonical_equiv_GBs
+        per_launch = cb0 / n0
         avg_s = ms0 * 1e-3 / n0
-        achieved = per_launch_bytes / avg_s / 1e9
+        achieved = per_launch / avg_s / 1e9
         # the committed PMC traffic is per launch of the single-GPU pass; a
         # rank's row block moves a fraction of it, so it is not reused there
-        kname = KERNEL_IDS.get((kind, lvl)) if (N, L, args.nsmooth, args.smoother, args.fuse,
-                                                world) == (16384, 9, 3, 0, 3, 1) else None
-        traffic = None
-        if kname:
-            kname, traffic = lookup_traffic(kname)
+        ids = KERNEL_IDS.get((kind, lvl)) if (N, L, args.nsmooth, args.smoother, args.fuse,
+                                              world) == (16384, 9, 3, 0, 3, 1) else None
+        kname, traffic, tsrc = (None, None, "no committed PMC profile for this configuration")
+        if ids:
+            kname, traffic, tsrc = lookup_traffic(ids)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": f"{_lib.KERNEL_NAMES[kind]} level {lvl}"
                           + (f" = {kname}" if kname else ""),
-                "per_launch_bytes": per_launch_bytes, "avg_launch_ms": round(avg_s * 1e3, 4)}
+                "compulsory_bytes_per_launch": per_launch,
+                "avg_launch_ms": round(avg_s * 1e3, 4),
+                "canonical_bytes_per_launch": b0 / n0,
+                "canonical_equiv_GBs": round(b0 / n0 / avg_s / 1e9, 1)}
         if traffic:
             # measured HBM bytes (rocprofv3 PMC, profiles/) / live mean duration
+            roof["traffic_source"] = tsrc
             roof["hbm_GBs"] = round(traffic / avg_s / 1e9, 1)
             roof["hbm_frac"] = round(traffic / avg_s / 1e9 / HBM_PEAK_GBS, 4)
+            roof["traffic_over_compulsory"] = round(traffic / per_launch, 3)
+        else:
+            roof["traffic_null_reason"] = tsrc
 
     value = (N - 1) ** 2 * args.steps / elapsed
     # SURVEY 8d secondary metric: RB-GS point updates per second
@@ -265,6 +348,7 @@ def main():
         # over the latter
         roof["copy_ceiling_GBs"] = round(_lib.stream_bandwidth(1 << 30, 1, 10), 1)
         roof["stream5_ceiling_GBs"] = round(_lib.stream_bandwidth(1 << 30, 4, 10), 1)
+        roof["achieved_frac_of_stream5"] = round(roof["achieved"] / roof["stream5_ceiling_GBs"], 4)
         if "hbm_GBs" in roof:
             roof["hbm_frac_of_stream5"] = round(roof["hbm_GBs"] / roof["stream5_ceiling_GBs"], 4)
     out = {
@@ -273,7 +357,7 @@ def main():
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "smoother_point_updates_per_s": smoother_pts * args.steps / elapsed,
-        "scaling": "weak" if (args.weak or world == 1) else "strong",
+        "scaling": "single" if world == 1 else ("weak" if args.weak else "strong"),
         "vs_baseline": None, "dtype": "f64",
         "data": "synthetic: the reference problem (Gaussian u0, rotating velocity), "
                 "generated on the host with glibc libm",

@@ -80,12 +80,15 @@ _SIGS = {
     "mgx_profile_enable": (_I, [_vp, _I]),
     "mgx_profile_reset": (_I, [_vp]),
     "mgx_profile_get": (_I, [_vp, _I, _I, C.POINTER(_L), _dp, _dp]),
+    "mgx_profile_get_ex": (_I, [_vp, _I, _I, C.POINTER(_L), _dp, _dp, _dp]),
     "mgx_set_tuning": (_I, [C.c_char_p, _L]),
     "mgx_stream_bandwidth": (_I, [_L, _I, _I, _dp]),
     "mgx_dist_unique_id": (_I, [_vp]),
     "mgx_create_dist": (_I, [C.POINTER(_vp), _L, _I, _D, _D, C.POINTER(Options), _I, _I, _vp]),
     "mgx_create_local_dist": (_I, [C.POINTER(_vp), _L, _I, _D, _D, C.POINTER(Options), _I]),
     "mgx_partition": (_I, [_L, _I, _I, _I, _I, C.POINTER(_I), C.POINTER(_I), C.POINTER(_I)]),
+    "mgx_exchange_plan": (_I, [_L, _I, _I, _I, _I, C.POINTER(_I), C.POINTER(_I), _I]),
+    "mgx_gather_plan": (_I, [_L, _I, _I, _I, C.POINTER(_I), C.POINTER(_I), C.POINTER(_I)]),
     "mgx_dist_info": (_I, [_vp, C.POINTER(_I), C.POINTER(_I), C.POINTER(_I)]),
     "mgx_dist_rows": (_I, [_vp, _I, C.POINTER(_I), C.POINTER(_I)]),
     "mgx_upload_rows": (_I, [_vp, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp)]),

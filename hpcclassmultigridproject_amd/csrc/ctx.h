@@ -45,7 +45,8 @@ struct Level {
 
 struct ProfRec {
     int kind, level;
-    double bytes;
+    double bytes;    // canonical algorithmic bytes (SURVEY 8d per-op model)
+    double cbytes;   // compulsory bytes: every array the launch reads or writes, once
     hipEvent_t e0, e1;
 };
 
@@ -73,6 +74,7 @@ struct mgx_ctx {
     std::vector<hipEvent_t> pool;
     double sum_ms[MGX_K_COUNT][64] = {};
     double sum_bytes[MGX_K_COUNT][64] = {};
+    double sum_cbytes[MGX_K_COUNT][64] = {};
     long count[MGX_K_COUNT][64] = {};
 };
 
@@ -81,8 +83,11 @@ namespace mgxi {
 hipEvent_t take_event(mgx_ctx *c);
 
 // Launch helper: records HIP events around the launch when profiling is on.
+// bytes: canonical algorithmic bytes of the reference ops the launch does
+// (SURVEY 8d); cbytes: its compulsory bytes (each array it must read or write,
+// once) -- the roofline denominator of a fused pass.
 template <class F>
-int launch(mgx_ctx *c, int kind, int level, double bytes, F &&f) {
+int launch(mgx_ctx *c, int kind, int level, double bytes, double cbytes, F &&f) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const bool rec = c->prof == 1 || (c->prof == 2 && level == 0);
     if (rec) {
@@ -94,9 +99,14 @@ int launch(mgx_ctx *c, int kind, int level, double bytes, F &&f) {
     CHK(check_launch("kernel launch"));
     if (rec && e0 && e1) {
         (void)hipEventRecord(e1, c->stream);
-        c->pending.push_back({kind, level, bytes, e0, e1});
+        c->pending.push_back({kind, level, bytes, cbytes, e0, e1});
     }
     return MGX_OK;
+}
+// single-op launches: canonical == compulsory
+template <class F>
+int launch(mgx_ctx *c, int kind, int level, double bytes, F &&f) {
+    return launch(c, kind, level, bytes, bytes, static_cast<F &&>(f));
 }
 
 int prof_flush(mgx_ctx *c);

@@ -94,6 +94,16 @@ static int plan_la(long n0, int L, int world) {
     return la;
 }
 
+static int ghost_width(int l) { return l == 0 ? kGhostFine : kGhost; }
+
+// allocated rows [lo, hi] of `rank` on level l: owned + ghosts, clipped
+static void alloc_rows(long n0, int l, int world, int rank, int *ra, int *rb, int *lo, int *hi) {
+    plan_rows(n0, l, world, rank, ra, rb);
+    const int g = ghost_width(l);
+    *lo = std::max(0, *ra - g);
+    *hi = (int)std::min<long>(n0 >> l, (long)*rb - 1 + g);
+}
+
 void dist_free(mgx_ctx *c) {
     Dist *d = c->dist;
     if (!d) return;
@@ -115,10 +125,22 @@ void dist_free(mgx_ctx *c) {
     c->dist = nullptr;
 }
 
+static int plan_check(long n0, int l, int world);
+
+// The all-gather into the first replicated level la: rank r contributes rows
+// [r*q, (r+1)*q), q = n_la / world (what its restriction from its level la-1
+// block writes; row n_la, the boundary, is never read), in place, rank-major.
+static void gather_rows(long n0, int la, int world, int rank, long *row0, long *rows) {
+    const long q = (n0 >> la) / world;
+    *row0 = rank * q;
+    *rows = q;
+}
+
 static int build_dist(mgx_ctx *c, int world, const std::vector<int> &ranks) {
     Dist *d = c->dist;
     d->world = world;
     d->la = plan_la(c->N, c->L, world);
+    for (int l = 0; l < d->la; ++l) CHK(plan_check(c->N, l, world));
     HIPCHK(hipHostMalloc(&d->hsum, sizeof(double) * 8));
     for (int r : ranks) {
         Part p;
@@ -129,10 +151,7 @@ static int build_dist(mgx_ctx *c, int world, const std::vector<int> &ranks) {
             L.n = c->N >> l;
             L.pitch = mgx::tower_pitch(L.n);
             L.coef = mgx::make_coef(c->dt, c->nu, h);
-            plan_rows(c->N, l, world, r, &L.ra, &L.rb);
-            const int g = l == 0 ? kGhostFine : kGhost;
-            L.lo = std::max(0, L.ra - g);
-            L.hi = (int)std::min<long>(L.n, (long)L.rb - 1 + g);
+            alloc_rows(c->N, l, world, r, &L.ra, &L.rb, &L.lo, &L.hi);
             const bool third = l == 0 && L.n >= kCrossMinN;
             double **bufs[6] = {&L.u[0], &L.u[1], &L.rhs, &L.v1, &L.v2, &L.u[2]};
             for (double **b : bufs) {
@@ -165,6 +184,74 @@ static double *field(const PLevel &L, Field f) {
     }
 }
 
+// ---- exchange plan.  ONE host-side description of every ghost-row transfer,
+// consumed by both transports: RCCL posts each entry as an ncclSend of its
+// send rows + an ncclRecv into its recv rows; the local (virtual-rank)
+// transport pairs each entry with the peer's entry for this rank and copies
+// sender rows -> receiver rows after checking that the two agree.  So the
+// single-GPU parity tests execute exactly the offsets / counts the RCCL ranks
+// post, and tests/test_capi.py checks the plan's symmetry on the CPU
+// (mgx_exchange_plan).  Rows are global row indices of the level.
+struct Xfer {
+    int peer;
+    int send_row, send_rows;   // send rows [send_row, +send_rows) to peer
+    int recv_row, recv_rows;   // receive rows [recv_row, +recv_rows) from it
+};
+
+// Ghost rows of level l of `rank`: [lo, ra) come from rank-1 (its last owned
+// rows), [rb, hi] from rank+1 (its first owned rows); it sends each
+// neighbour the rows that neighbour's ghosts mirror.
+static void ghost_plan(long n0, int l, int world, int rank, std::vector<Xfer> &out) {
+    out.clear();
+    if (world <= 1) return;
+    int ra, rb, lo, hi;
+    alloc_rows(n0, l, world, rank, &ra, &rb, &lo, &hi);
+    for (int peer : {rank - 1, rank + 1}) {
+        if (peer < 0 || peer >= world) continue;
+        int pa, pb, plo, phi;
+        alloc_rows(n0, l, world, peer, &pa, &pb, &plo, &phi);
+        Xfer x;
+        x.peer = peer;
+        if (peer < rank) {   // its upper ghosts [pb, phi] = my first owned rows
+            x.send_row = pb;
+            x.send_rows = phi - pb + 1;
+            x.recv_row = lo;
+            x.recv_rows = ra - lo;
+        } else {             // its lower ghosts [plo, pa) = my last owned rows
+            x.send_row = plo;
+            x.send_rows = pa - plo;
+            x.recv_row = rb;
+            x.recv_rows = hi - rb + 1;
+        }
+        out.push_back(x);
+    }
+}
+
+// The plans of all ranks agree pairwise (what i sends j is what j receives
+// from i: same global rows, same count), sends read only owned rows, receives
+// land only in allocated ghost rows.
+static int plan_check(long n0, int l, int world) {
+    std::vector<std::vector<Xfer>> P(world);
+    for (int r = 0; r < world; ++r) ghost_plan(n0, l, world, r, P[r]);
+    for (int r = 0; r < world; ++r) {
+        int ra, rb, lo, hi;
+        alloc_rows(n0, l, world, r, &ra, &rb, &lo, &hi);
+        for (const Xfer &x : P[r]) {
+            if (x.send_rows <= 0 || x.send_row < ra || x.send_row + x.send_rows > rb)
+                return fail(MGX_E_INTERNAL, "exchange plan: send outside the owned rows");
+            if (x.recv_rows <= 0 || x.recv_row < lo || x.recv_row + x.recv_rows > hi + 1 ||
+                (x.recv_row < rb && x.recv_row + x.recv_rows > ra))
+                return fail(MGX_E_INTERNAL, "exchange plan: receive outside the ghost rows");
+            const Xfer *y = nullptr;
+            for (const Xfer &z : P[x.peer])
+                if (z.peer == r) y = &z;
+            if (!y || y->recv_row != x.send_row || y->recv_rows != x.send_rows)
+                return fail(MGX_E_INTERNAL, "exchange plan: peers disagree");
+        }
+    }
+    return MGX_OK;
+}
+
 // Refresh the ghost rows of the listed (level, field)s from the neighbouring
 // ranks; over RCCL all of them go in ONE group (one latency, not one each).
 struct XF {
@@ -174,22 +261,20 @@ struct XF {
 
 static int exchange_rows(mgx_ctx *c, std::initializer_list<XF> xs) {
     Dist *d = c->dist;
+    std::vector<Xfer> plan;
     if (d->local) {
+        // part i's send to j lands where j's plan receives from i (the plan is
+        // checked pairwise at context creation: plan_check)
         for (const XF &x : xs)
             for (size_t i = 0; i < d->parts.size(); ++i) {
-                PLevel &L = d->parts[i].lv[x.l];
+                const PLevel &L = d->parts[i].lv[x.l];
                 const long P = L.pitch;
-                double *dst = field(L, x.f);
-                if (i > 0) {   // rows [lo, ra) from rank i-1
-                    const PLevel &A = d->parts[i - 1].lv[x.l];
-                    HIPCHK(hipMemcpyAsync(dst + (long)L.lo * P, field(A, x.f) + (long)L.lo * P,
-                                          sizeof(double) * (L.ra - L.lo) * P,
-                                          hipMemcpyDeviceToDevice, c->stream));
-                }
-                if (i + 1 < d->parts.size()) {   // rows [rb, hi] from rank i+1
-                    const PLevel &B = d->parts[i + 1].lv[x.l];
-                    HIPCHK(hipMemcpyAsync(dst + (long)L.rb * P, field(B, x.f) + (long)L.rb * P,
-                                          sizeof(double) * (L.hi - L.rb + 1) * P,
+                ghost_plan(c->N, x.l, d->world, d->parts[i].rank, plan);
+                for (const Xfer &t : plan) {
+                    PLevel &R = d->parts[t.peer].lv[x.l];
+                    HIPCHK(hipMemcpyAsync(field(R, x.f) + (long)t.send_row * P,
+                                          field(L, x.f) + (long)t.send_row * P,
+                                          sizeof(double) * (size_t)t.send_rows * P,
                                           hipMemcpyDeviceToDevice, c->stream));
                 }
             }
@@ -201,21 +286,14 @@ static int exchange_rows(mgx_ctx *c, std::initializer_list<XF> xs) {
         PLevel &L = p.lv[x.l];
         const long P = L.pitch;
         double *a = field(L, x.f);
-        if (r == ncclSuccess && p.rank > 0) {
-            const size_t cnt = (size_t)(L.ra - L.lo) * P;
-            r = ncclSend(a + (long)L.ra * P, cnt, ncclDouble, p.rank - 1, d->comm, c->stream);
+        ghost_plan(c->N, x.l, d->world, p.rank, plan);
+        for (const Xfer &t : plan) {
+            if (r != ncclSuccess) break;
+            r = ncclSend(a + (long)t.send_row * P, (size_t)t.send_rows * P, ncclDouble, t.peer,
+                         d->comm, c->stream);
             if (r == ncclSuccess)
-                r = ncclRecv(a + (long)L.lo * P, cnt, ncclDouble, p.rank - 1, d->comm,
-                             c->stream);
-        }
-        if (r == ncclSuccess && p.rank < d->world - 1) {
-            const int g = L.hi - L.rb + 1;
-            const size_t cnt = (size_t)g * P;
-            r = ncclSend(a + (long)(L.rb - g) * P, cnt, ncclDouble, p.rank + 1, d->comm,
-                         c->stream);
-            if (r == ncclSuccess)
-                r = ncclRecv(a + (long)L.rb * P, cnt, ncclDouble, p.rank + 1, d->comm,
-                             c->stream);
+                r = ncclRecv(a + (long)t.recv_row * P, (size_t)t.recv_rows * P, ncclDouble,
+                             t.peer, d->comm, c->stream);
         }
     }
     const ncclResult_t re = ncclGroupEnd();   // always close the group
@@ -228,10 +306,15 @@ static int exchange_rows(mgx_ctx *c, std::initializer_list<XF> xs) {
 static int exchange(mgx_ctx *c, std::initializer_list<XF> xs) {
     if (c->dist->world == 1 || xs.size() == 0) return MGX_OK;
     int rc = MGX_OK;
+    // bytes moved by the parts this process holds: every row sent is read once
+    // and written once
     double bytes = 0;
+    std::vector<Xfer> plan;
     for (const XF &x : xs)
-        bytes += 16.0 * (c->dist->parts[0].lv[x.l].ra - c->dist->parts[0].lv[x.l].lo) *
-                 c->dist->parts[0].lv[x.l].pitch * c->dist->parts.size();
+        for (const Part &p : c->dist->parts) {
+            ghost_plan(c->N, x.l, c->dist->world, p.rank, plan);
+            for (const Xfer &t : plan) bytes += 16.0 * t.send_rows * p.lv[x.l].pitch;
+        }
     CHK(launch(c, MGX_K_HALO, xs.begin()->l, bytes, [&] { rc = exchange_rows(c, xs); }));
     return rc;
 }
@@ -242,24 +325,26 @@ static int exchange(mgx_ctx *c, int l, Field f) { return exchange(c, {XF{l, f}})
 // of the full array in its sub-context; make them whole everywhere.
 static int gather_rhs(mgx_ctx *c) {
     Dist *d = c->dist;
-    const long nl = c->N >> d->la;
-    const long q = nl / d->world;   // rows per rank; row nl (boundary) is never read
     if (d->world > 1) {
+        long row0, q;
         if (d->local) {
             for (auto &dst : d->parts)
                 for (auto &src : d->parts) {
                     if (&dst == &src) continue;
-                    const long P = dst.sub->lv[0].pitch, off = (long)src.rank * q * P;
+                    gather_rows(c->N, d->la, d->world, src.rank, &row0, &q);
+                    const long P = dst.sub->lv[0].pitch, off = row0 * P;
                     HIPCHK(hipMemcpyAsync(dst.sub->lv[0].rhs + off, src.sub->lv[0].rhs + off,
                                           sizeof(double) * q * P, hipMemcpyDeviceToDevice,
                                           c->stream));
                 }
         } else {
             Part &p = d->parts[0];
+            gather_rows(c->N, d->la, d->world, p.rank, &row0, &q);
             const long P = p.sub->lv[0].pitch;
             double *rhs = p.sub->lv[0].rhs;
-            NCCLCHK(ncclAllGather(rhs + (long)p.rank * q * P, rhs, (size_t)q * P, ncclDouble,
-                                  d->comm, c->stream));
+            // in place: the send buffer is the receive buffer + rank * count
+            NCCLCHK(ncclAllGather(rhs + row0 * P, rhs, (size_t)q * P, ncclDouble, d->comm,
+                                  c->stream));
         }
     }
     for (auto &p : d->parts) p.sub->lv[0].zero = true;   // u[la] = 0 (multigrid.cpp:77)
@@ -348,8 +433,14 @@ static int smooth(mgx_ctx *c, int l, bool prolong, bool restrict_, bool norm) {
             A.norm_out = p.dsum;
             A.norm_sqrt = false;
             double bytes = 40.0 * k * L.Mown();
+            const double Mc = L.Mown() / 4;
+            if (pr) bytes += 32.0 * L.Mown() + 8.0 * Mc;
+            if (rs) bytes += 40.0 * L.Mown() + 24.0 * Mc;
+            if (nm) bytes += 48.0 * L.Mown();
+            const double cbytes = 8.0 * ((zero ? 4.0 : 5.0) * L.Mown() +
+                                         ((pr ? 1 : 0) + (rs ? 1 : 0)) * Mc);
             int blocks = 0;
-            CHK(launch(c, pr ? MGX_K_PSMOOTH : MGX_K_GS, l, bytes,
+            CHK(launch(c, pr ? MGX_K_PSMOOTH : MGX_K_GS, l, bytes, cbytes,
                        [&] { blocks = mgx::launch_smooth(A, k, mode, c->stream); }));
             if (blocks < 0) return fail(MGX_E_ARG, "launch_smooth: unsupported sweeps/mode");
             L.cur = L.nxt();
@@ -454,8 +545,9 @@ static int dist_cross(mgx_ctx *c, bool store_post) {
         A.hi = L.hi;
         const int k = c->opt.nsmooth;
         const double bytes = (32.0 + 40.0 * k + 48.0 + 40.0 * k + 40.0) * L.Mown() + 32.0 * Mc;
+        const double cbytes = 8.0 * ((store_post ? 6.0 : 5.0) * L.Mown() + 2.0 * Mc);
         int blocks = 0;
-        CHK(launch(c, MGX_K_XSMOOTH, 0, bytes,
+        CHK(launch(c, MGX_K_XSMOOTH, 0, bytes, cbytes,
                    [&] { blocks = mgx::launch_xsmooth(A, k, c->stream); }));
         if (blocks < 0) return fail(MGX_E_ARG, "launch_xsmooth: unsupported sweeps / block");
         L.cur = P;
@@ -502,7 +594,7 @@ int dist_residual_norm(mgx_ctx *c, double *norm) {
     CHK(exchange(c, 0, kU));
     for (auto &p : d->parts) {
         PLevel &L = p.lv[0];
-        CHK(launch(c, MGX_K_RESNORM, 0, 48.0 * L.Mown(), [&] {
+        CHK(launch(c, MGX_K_RESNORM, 0, 48.0 * L.Mown(), 32.0 * L.Mown(), [&] {
             mgx::launch_residual_norm(L.U(), L.F(L.rhs), L.F(L.v1), L.F(L.v2), L.n, L.pitch,
                                       L.coef, c->partials, p.dsum, c->stream, L.ra, L.rb,
                                       /*take_sqrt=*/false);
@@ -785,6 +877,40 @@ int mgx_partition(long n, int maxlvl, int world, int rank, int level, int *ra, i
         if (ra) *ra = a;
         if (rb) *rb = b;
     }
+    return MGX_OK;
+}
+
+int mgx_exchange_plan(long n, int maxlvl, int world, int rank, int level, int *count,
+                      int *xfers, int cap) {
+    if (n < 2 || (n & (n - 1)) || maxlvl < 1 || world < 1 || (world & (world - 1)) ||
+        rank < 0 || rank >= world || level < 0 || level >= maxlvl || !count)
+        return fail(MGX_E_ARG, "mgx_exchange_plan: bad args");
+    std::vector<Xfer> plan;
+    if (level < plan_la(n, maxlvl, world)) ghost_plan(n, level, world, rank, plan);
+    *count = (int)plan.size();
+    if ((int)plan.size() > cap || (!xfers && !plan.empty()))
+        return fail(MGX_E_ARG, "mgx_exchange_plan: output too small");
+    for (size_t i = 0; i < plan.size(); ++i) {
+        int *o = xfers + 5 * i;
+        o[0] = plan[i].peer;
+        o[1] = plan[i].send_row;
+        o[2] = plan[i].send_rows;
+        o[3] = plan[i].recv_row;
+        o[4] = plan[i].recv_rows;
+    }
+    return MGX_OK;
+}
+
+int mgx_gather_plan(long n, int maxlvl, int world, int rank, int *level, int *row0,
+                    int *rows) {
+    if (n < 2 || maxlvl < 1 || world < 1 || rank < 0 || rank >= world)
+        return fail(MGX_E_ARG, "mgx_gather_plan: bad args");
+    const int la = plan_la(n, maxlvl, world);
+    long r0, q;
+    gather_rows(n, la, world, rank, &r0, &q);
+    if (level) *level = la;
+    if (row0) *row0 = (int)r0;
+    if (rows) *rows = (int)q;
     return MGX_OK;
 }
 

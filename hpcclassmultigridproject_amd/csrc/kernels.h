@@ -107,10 +107,6 @@ int launch_xsmooth(const XArgs &a, int sweeps, hipStream_t s);
 // Cross pass: 1 = interior strips run the unguarded march (default), 0 = all guarded.
 void set_xfast(long v);
 long get_xfast();
-// Cross pass: 1 = its edge kernel runs on a side stream, overlapping the
-// interior kernel's tail (joined before the next launch on the caller's stream).
-void set_xoverlap(long v);
-long get_xoverlap();
 // Levels with n <= tile_max_n use the 2-D tile form of the fused pass (small
 // levels: latency bound), larger ones the row march.  Default 2048, or the
 // MGX_TILE_MAX_N environment variable.
@@ -132,11 +128,6 @@ long get_march_order();
 // longer segments amortise the warm-up rows, more keep more waves in flight.
 void set_march_min_rows(long v);
 long get_march_min_rows();
-// Workgroup width (lanes) of the row march on levels with n >= 4096: 128 or 256.
-void set_march_block(long v);
-void set_march_kernel(long v);
-long get_march_kernel();
-long get_march_block();
 // One colour, in place (two launches make a sweep).  Reference for A/B timing.
 void launch_gs_colour(double *u, const double *rhs, const double *v1, const double *v2,
                       long n, long pitch, Coef c, int colour, hipStream_t s);

@@ -138,40 +138,48 @@ __global__ __launch_bounds__(kFinalThreads) void k_norm_final(const double *part
 
 // ============================================================ reference layout
 // One lane per point, pitch n+1.  These back the gs.h-mirror entry points.
+// 64-bit indexing throughout: at N = 65536 an array holds 4.3e9 elements
+// (where the reference's int index math overflows).  Rows go over
+// blockIdx.y with a grid stride (gridDim.y is capped at kMaxGridY).
+constexpr long kMaxGridY = 32768;
 
 __global__ __launch_bounds__(256) void k_raw_gs_colour(double *u, const double *rhs,
                                                        const double *v1, const double *v2,
                                                        long n, Coef c, int colour) {
     const long w = n + 1;
-    const long i = 1 + blockIdx.y;
-    // points of this colour in row i: j = j0, j0+2, ... (gs.cpp:121-184)
-    const long j0 = (colour == 0) ? (2 - (i & 1)) : (1 + (i & 1));
-    const long j = j0 + 2 * ((long)blockIdx.x * blockDim.x + threadIdx.x);
-    if (i >= n || j >= n) return;
-    const long p = i * w + j;
-    u[p] = gs_point(rhs[p], v1[p], v2[p], u[p - w], u[p - 1], u[p + w], u[p + 1], c);
+    for (long i = 1 + blockIdx.y; i < n; i += gridDim.y) {
+        // points of this colour in row i: j = j0, j0+2, ... (gs.cpp:121-184)
+        const long j0 = (colour == 0) ? (2 - (i & 1)) : (1 + (i & 1));
+        const long j = j0 + 2 * ((long)blockIdx.x * blockDim.x + threadIdx.x);
+        if (j >= n) continue;
+        const long p = i * w + j;
+        u[p] = gs_point(rhs[p], v1[p], v2[p], u[p - w], u[p - 1], u[p + w], u[p + 1], c);
+    }
 }
 
 __global__ __launch_bounds__(256) void k_raw_residual(double *res, const double *u,
                                                       const double *rhs, const double *v1,
                                                       const double *v2, long n, Coef c) {
     const long w = n + 1;
-    const long i = 1 + blockIdx.y;
     const long j = 1 + (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || j >= n) return;
-    const long p = i * w + j;
-    res[p] = res_point(rhs[p], v1[p], v2[p], u[p], u[p - w], u[p - 1], u[p + w], u[p + 1], c);
+    if (j >= n) return;
+    for (long i = 1 + blockIdx.y; i < n; i += gridDim.y) {
+        const long p = i * w + j;
+        res[p] = res_point(rhs[p], v1[p], v2[p], u[p], u[p - w], u[p - 1], u[p + w], u[p + 1],
+                           c);
+    }
 }
 
 __global__ __launch_bounds__(256) void k_raw_rhs(double *rhs, const double *u,
                                                  const double *v1, const double *v2, long n,
                                                  Coef c) {
     const long w = n + 1;
-    const long i = 1 + blockIdx.y;
     const long j = 1 + (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || j >= n) return;
-    const long p = i * w + j;
-    rhs[p] = rhs_point(v1[p], v2[p], u[p], u[p - w], u[p - 1], u[p + w], u[p + 1], c);
+    if (j >= n) return;
+    for (long i = 1 + blockIdx.y; i < n; i += gridDim.y) {
+        const long p = i * w + j;
+        rhs[p] = rhs_point(v1[p], v2[p], u[p], u[p - w], u[p - 1], u[p + w], u[p + 1], c);
+    }
 }
 
 // Fine point (I,J) of the (2n+1)^2 output from coarse (i,j)=(I/2,J/2) by the
@@ -192,28 +200,20 @@ __device__ __forceinline__ double prolong_value(const double *u, long w, long I,
 __global__ __launch_bounds__(256) void k_raw_prolongation(double *up, const double *u,
                                                           long n) {
     const long W = 2 * n + 1;
-    const long I = blockIdx.y;
     const long J = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (I >= W || J >= W) return;
-    up[I * W + J] = prolong_value(u, n + 1, I, J);
+    if (J >= W) return;
+    for (long I = blockIdx.y; I < W; I += gridDim.y) up[I * W + J] = prolong_value(u, n + 1, I, J);
 }
 
-__global__ __launch_bounds__(256) void k_injection(double *dst, long dpitch,
-                                                   const double *src, long spitch, long m) {
-    const long I = blockIdx.y;
-    const long J = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (I >= m || J >= m) return;
-    dst[I * dpitch + J] = src[2 * I * spitch + 2 * J];
-}
-
-// Injection of a block of coarse rows: dst row I, col J <- src row 2I, col 2J.
+// Injection of a block of coarse rows: dst row I, col J <- src row 2I, col 2J
+// (restriction, gs.cpp:283; the tower build, multigrid.cpp:148-160).
 __global__ __launch_bounds__(256) void k_injection_rows(double *dst, long dpitch,
                                                         const double *src, long spitch,
                                                         long rows, long cols) {
-    const long I = blockIdx.y;
     const long J = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (I >= rows || J >= cols) return;
-    dst[I * dpitch + J] = src[2 * I * spitch + 2 * J];
+    if (J >= cols) return;
+    for (long I = blockIdx.y; I < rows; I += gridDim.y)
+        dst[I * dpitch + J] = src[2 * I * spitch + 2 * J];
 }
 
 // Interior sum of squares, rows split over the grid; deterministic per block.
@@ -455,7 +455,20 @@ struct RowData {
 // The sign of a/d is sign(a) xor sign(d), also for a = +-0 (where the fma
 // chain alone would return +0 for a = -0): one v_xor + v_bfi on the high word
 // instead of a compare and two selects.
+//
+// POSD (the diagonal d > 0, as for every nu <= 0): the same correction with
+// the residual negated, rn = q0*d - a and q = fma(-rn, y, q0), is the same
+// rounded value for every a != 0 (RN is symmetric) and gets the zero sign
+// right by itself: a = -0 gives q0 = -0, rn = +0, q = -0 + -0 = -0; a = +0
+// gives +0.  (For d < 0 it would not: a = +0 -> +0, not -0.)  Two integer ops
+// fewer per point update; the launchers route d <= 0 to the general form.
+template <bool POSD = false>
 __device__ __forceinline__ double div_diag(double a, const Coef &c) {
+    if (POSD) {
+        const double q0 = a * c.rdgs;
+        const double rn = __builtin_fma(q0, c.dgs, -a);
+        return __builtin_fma(-rn, c.rdgs, q0);
+    }
     const double q0 = a * c.rdgs;
     const double r = __builtin_fma(-q0, c.dgs, a);
     const double q = __builtin_fma(r, c.rdgs, q0);
@@ -485,221 +498,6 @@ struct SmoothCfg {
     static constexpr int NR = E + 3;                     // LDS ring rows
     static constexpr int NS = S + 2;                     // register ring rows / unroll
 };
-
-template <int BLOCK, int K, int MODE>
-__global__ __launch_bounds__(BLOCK) void k_smooth(
-    const double *__restrict__ uin, double *__restrict__ uout, const double *__restrict__ rhs,
-    const double *__restrict__ v1, const double *__restrict__ v2, const double *__restrict__ uc,
-    long pitchc, double *__restrict__ rhsc, double *__restrict__ partials, int n, long pitch,
-    int strips, long units_per_wg, Coef c, int ra, int rb, int lo, int hi) {
-    using C = SmoothCfg<K, MODE>;
-    constexpr int S = C::S, E = C::E, H = C::H, NR = C::NR, NS = C::NS;
-    // LDS row = two planes, even and odd columns: lane l's pair (2c, 2c+1)
-    // sits at index l+1 of each, so every stage and residual access is a
-    // unit-stride 8-B word per lane (bank-conflict free; the interleaved
-    // layout's 16-B lane stride cost ~28% of LDS cycles in conflicts)
-    constexpr int LP = BLOCK + 2;
-    constexpr int W = 2 * (BLOCK - 2 * H);
-    __shared__ __attribute__((aligned(16))) double ring[NR][2][LP];
-
-    const int l = threadIdx.x;
-    const int nrows = rb - ra;
-    const long total = (long)strips * nrows;
-    long start = (long)blockIdx.x * units_per_wg;
-    const long end = min(total, start + units_per_wg);
-    const int nc = n >> 1;
-    double acc = 0.0;   // NORM partial
-
-    while (start < end) {
-        const int strip = (int)(start / nrows);
-        const int a = ra + (int)(start % nrows);
-        const int b = (int)min((long)rb, (long)a + (end - start));
-        start += b - a;
-
-        const int j0 = strip * W;
-        const int c0 = j0 - 2 * H + 2 * l;   // lane column (32-bit: the row base is scalar)
-        const bool act = c0 >= 0 && c0 <= n;
-        const bool keep = act && l >= H && l < BLOCK - H;
-        // per-lane interior flags of the two columns of the pair
-        const bool in0 = act && c0 >= 1 && c0 <= n - 1;
-        const bool in1 = act && c0 + 1 <= n - 1;
-        const int pl = l + 1;   // plane index of this lane's pair
-
-        // Prefetched u rows (+ coarse operands of their prolongation): row R
-        // lives in set R & 1 from its load at step R-5 to its LDS store at step
-        // R-3 (prefetch distance 2).  s == p (mod 2), so the set is static.
-        struct UPre {
-            double2 X;
-            double q00, q01, q10, q11;
-        };
-        UPre up[2];
-        up[0] = up[1] = UPre{make_double2(0.0, 0.0), 0.0, 0.0, 0.0, 0.0};
-        // Loads are issued unconditionally, with row and column clamped into
-        // the array: a conditional load makes the waitcnt pass fall back to
-        // vmcnt(0) and drain the whole prefetch queue.  Values loaded for rows
-        // or lanes outside the domain are never used.
-        const int cl = min(max(c0, 0), (int)pitch - 2);   // clamped lane column
-        const int jl = cl >> 1;                            // its coarse column
-        const int j1 = (jl + 1 <= nc) ? 1 : 0;
-        auto load_u = [&](int R, UPre &u) {
-            if (C::ZERO) return;
-            const int Rc = min(max(R, lo), hi);
-            u.X = ld2s((uin + (long)Rc * pitch) + cl);
-            if (C::PROL) {
-                // branch-free: even rows read coarse row R/2 twice (cache hits)
-                const double *p0 = (uc + (long)(Rc >> 1) * pitchc) + jl;
-                const double *p1 = p0 + ((Rc & 1) ? pitchc : 0);
-                u.q00 = p0[0];
-                u.q01 = p0[j1];
-                u.q10 = p1[0];
-                u.q11 = p1[j1];
-            }
-        };
-        auto put_u = [&](int R, int sl, const UPre &u) {
-            double2 v = u.X;
-            if (C::ZERO) v = make_double2(0.0, 0.0);
-            if (C::PROL && act && R >= 0 && R <= n) {
-                double2 pr;
-                const double q01 = j1 ? u.q01 : 0.0;
-                const double q11 = j1 ? u.q11 : 0.0;
-                if (!(R & 1)) {
-                    pr.x = u.q00;
-                    pr.y = (u.q00 + q01) / 2;
-                } else {
-                    pr.x = (u.q00 + u.q10) / 2;
-                    pr.y = (u.q00 + u.q10 + q01 + q11) / 4;
-                }
-                v.x = v.x + pr.x;
-                v.y = v.y + pr.y;
-            }
-            ring[sl][0][pl] = v.x;
-            ring[sl][1][pl] = v.y;
-        };
-        auto load_rv = [&](int R, RowData &d) {
-            const long o = (long)min(max(R, lo), hi) * pitch;   // scalar row offset
-            d.r = ld2s((rhs + o) + cl);
-            d.x = ld2s((v1 + o) + cl);
-            d.y = ld2s((v2 + o) + cl);
-        };
-
-        const int s_first = a - E;
-        const int s_last = b + E - 3;
-        // align the first step to the unroll period NS (even): then the parity
-        // of s equals the parity of the unrolled copy index.  Leading extra
-        // steps only compute values outside the exact cone.
-        int s = s_first >= 0 ? (s_first / NS) * NS : -(((-s_first) + NS - 1) / NS) * NS;
-        s = __builtin_amdgcn_readfirstlane(s);
-        // ring slot of row s: base = s mod NR (scalar)
-        int base = ((s % NR) + NR) % NR;
-
-        RowData rd[NS];
-#pragma unroll
-        for (int q = 0; q < NS; ++q) rd[q].r = rd[q].x = rd[q].y = make_double2(0.0, 0.0);
-        // prologue (s even): ring rows s..s+2; u rows s+3, s+4 in flight (sets 1,
-        // 0); rhs/v rows s+1, s+2 in rd[1], rd[2]
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            load_u(s + d, up[0]);
-            int sl = base + d;
-            sl -= sl >= NR ? NR : 0;
-            put_u(s + d, sl, up[0]);
-        }
-        load_u(s + 3, up[1]);
-        load_u(s + 4, up[0]);
-        load_rv(s + 1, rd[1]);
-        load_rv(s + 2, rd[2]);
-        __syncthreads();
-
-        for (;;) {
-#pragma unroll
-            for (int p = 0; p < NS; ++p) {
-                // slot(s + d) for d in [-E, 3], scalar
-                auto slot = [&](int d) {
-                    int t = base + d;
-                    if (d > 0) t -= t >= NR ? NR : 0;
-                    if (d < 0) t += t < 0 ? NR : 0;
-                    return t;
-                };
-                // (1) u row s+3 into the ring; its prefetch set takes u row s+5
-                put_u(s + 3, slot(3), up[(p + 1) & 1]);
-                load_u(s + 5, up[(p + 1) & 1]);
-                // (2) the S smoothing stages
-#pragma unroll
-                for (int h = 0; h < S; ++h) {
-                    const int r = s + 1 - h;
-                    // parity of r is static: s == p (mod 2)
-                    const int cs = ((p + 1 - h) & 1) ^ (h & 1);
-                    const bool inr = r >= 1 && r <= n - 1;
-                    if (inr && (cs ? in1 : in0)) {
-                        const RowData &d = rd[(p + 1 - h + 2 * NS) % NS];
-                        double(*row)[LP] = ring[slot(1 - h)];
-                        const double uN = ring[slot(-h)][cs][pl], uS = ring[slot(2 - h)][cs][pl];
-                        // west / east neighbours are in the other plane:
-                        // even column 2c: odd 2c-1 (pl-1), 2c+1 (pl);
-                        // odd column 2c+1: even 2c (pl), 2c+2 (pl+1)
-                        const double uW = row[cs ^ 1][pl - 1 + cs];
-                        const double uE = row[cs ^ 1][pl + cs];
-                        row[cs][pl] = gs_point_fast(cs ? d.r.y : d.r.x, cs ? d.x.y : d.x.x,
-                                                    cs ? d.y.y : d.y.x, uN, uW, uS, uE, c);
-                    }
-                    __syncthreads();
-                }
-                // (3) output row s+2-S is final
-                {
-                    const int ro = s + 2 - S;
-                    if (keep && ro >= a && ro < b)
-                        st2s((uout + (long)ro * pitch) + c0,
-                            make_double2(ring[slot(2 - S)][0][pl], ring[slot(2 - S)][1][pl]));
-                }
-                // (4) residual stage on row s+1-S
-                if (C::REST || C::NORM) {
-                    const int r = s + 1 - S;
-                    const RowData &d = rd[(p + 1 - S + 2 * NS) % NS];
-                    if (keep && r >= a && r < b && r >= 1 && r <= n - 1) {
-                        const double(*rm)[LP] = ring[slot(1 - S)];
-                        const double(*rn_)[LP] = ring[slot(-S)];
-                        const double(*rs_)[LP] = ring[slot(2 - S)];
-                        if (C::REST) {
-                            // even-even points only: r even (static), c0 = 2J
-                            if (((p + 1 - S) & 1) == 0 && in0 && c0 <= n - 2 && r <= n - 2) {
-                                const double res =
-                                    res_point(d.r.x, d.x.x, d.y.x, rm[0][pl], rn_[0][pl],
-                                              rm[1][pl - 1], rs_[0][pl], rm[1][pl], c);
-                                (rhsc + (long)(r >> 1) * pitchc)[c0 >> 1] = res;
-                            }
-                        } else {
-                            if (in0) {
-                                const double res =
-                                    res_point(d.r.x, d.x.x, d.y.x, rm[0][pl], rn_[0][pl],
-                                              rm[1][pl - 1], rs_[0][pl], rm[1][pl], c);
-                                acc += res * res;
-                            }
-                            if (in1) {
-                                const double res =
-                                    res_point(d.r.y, d.x.y, d.y.y, rm[1][pl], rn_[1][pl],
-                                              rm[0][pl], rs_[1][pl], rm[0][pl + 1], c);
-                                acc += res * res;
-                            }
-                        }
-                    }
-                }
-                // (5) rhs/v row s+3 into the slot of row s+1-S, whose last use
-                // (the residual stage, or stage S-1 one step ago) is done
-                load_rv(s + 3, rd[(p + 3) % NS]);
-                ++base;
-                base -= base >= NR ? NR : 0;
-                if (++s > s_last) goto done;
-            }
-        }
-    done:
-        __syncthreads();
-    }
-    if (C::NORM) {
-        __shared__ double red_lds[BLOCK / 64];
-        const double tot = block_sum(acc, red_lds);
-        if (l == 0) partials[blockIdx.x] = tot;
-    }
-}
 
 // Work of one march launch (k_wsmooth, k_xsmooth): up to 4 rectangles of
 // (strip group, row) units, enumerated group-major.  Region k covers strips
@@ -808,11 +606,12 @@ __device__ __forceinline__ double dpp_shl1(double v) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 // gs.cpp:130 / :75 with the velocity terms pre-scaled: t1 = v1*h/2, t2 = v2*h/2
+template <bool POSD = false>
 __device__ __forceinline__ double gs_point_t(double rhs, double t1, double t2, double uN,
                                              double uW, double uS, double uE, const Coef &c) {
     const double aa = c.rr * (c.nu - t2), bb = c.rr * (t2 + c.nu);
     const double cc = c.rr * (c.nu - t1), dd = c.rr * (t1 + c.nu);
-    return div_diag(rhs - cc * uN - aa * uW - dd * uS - bb * uE, c);
+    return div_diag<POSD>(rhs - cc * uN - aa * uW - dd * uS - bb * uE, c);
 }
 __device__ __forceinline__ double res_point_t(double rhs, double t1, double t2, double u,
                                               double uN, double uW, double uS, double uE,
@@ -1167,16 +966,17 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             // per SIMD: spills); guarded stages are branches, never CSE'd
             Coef cg = c;
             if (!GS) asm volatile("" : "+s"(cg.nu));
+            // (the unguarded kernel only runs with d > 0: xsmooth_inst)
             if (cs == 0) {
                 const double uW = dpp_shr1(ur[iR].y);
                 if (!GS || (inr && in0))
-                    ur[iR].x = gs_point_t(d.r.x, d.x.x, d.y.x, ur[iN].x, uW, ur[iS].x,
-                                          ur[iR].y, cg);
+                    ur[iR].x = gs_point_t<!GS>(d.r.x, d.x.x, d.y.x, ur[iN].x, uW, ur[iS].x,
+                                               ur[iR].y, cg);
             } else {
                 const double uE = dpp_shl1(ur[iR].x);
                 if (!GS || (inr && in1))
-                    ur[iR].y = gs_point_t(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x, ur[iS].y,
-                                          uE, cg);
+                    ur[iR].y = gs_point_t<!GS>(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x,
+                                               ur[iS].y, uE, cg);
             }
         };
 
@@ -1785,39 +1585,40 @@ inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }
 #define MGX_LAUNCH(kern, grid, block, s, ...) \
     hipLaunchKernelGGL((kern), (grid), (block), 0, (s), __VA_ARGS__)
 
+static unsigned grid_y(long rows) { return (unsigned)std::max<long>(1, std::min(rows, kMaxGridY)); }
+
 void launch_raw_gs_colour(double *u, const double *rhs, const double *v1, const double *v2,
                           long n, Coef c, int colour, hipStream_t s) {
     if (n < 2) return;
-    dim3 g(cdiv(n / 2, 256), (unsigned)(n - 1));
+    dim3 g(cdiv(n / 2, 256), grid_y(n - 1));
     MGX_LAUNCH(k_raw_gs_colour, g, dim3(256), s, u, rhs, v1, v2, n, c, colour);
 }
 void launch_raw_residual(double *res, const double *u, const double *rhs, const double *v1,
                          const double *v2, long n, Coef c, hipStream_t s) {
     if (n < 2) return;
-    dim3 g(cdiv(n - 1, 256), (unsigned)(n - 1));
+    dim3 g(cdiv(n - 1, 256), grid_y(n - 1));
     MGX_LAUNCH(k_raw_residual, g, dim3(256), s, res, u, rhs, v1, v2, n, c);
 }
 void launch_raw_rhs(double *rhs, const double *u, const double *v1, const double *v2, long n,
                     Coef c, hipStream_t s) {
     if (n < 2) return;
-    dim3 g(cdiv(n - 1, 256), (unsigned)(n - 1));
+    dim3 g(cdiv(n - 1, 256), grid_y(n - 1));
     MGX_LAUNCH(k_raw_rhs, g, dim3(256), s, rhs, u, v1, v2, n, c);
 }
 void launch_raw_prolongation(double *up, const double *u, long n, hipStream_t s) {
     const long W = 2 * n + 1;
-    dim3 g(cdiv(W, 256), (unsigned)W);
+    dim3 g(cdiv(W, 256), grid_y(W));
     MGX_LAUNCH(k_raw_prolongation, g, dim3(256), s, up, u, n);
 }
 void launch_injection(double *dst, long dst_pitch, const double *src, long src_pitch, long m,
                       hipStream_t s) {
-    dim3 g(cdiv(m, 256), (unsigned)m);
-    MGX_LAUNCH(k_injection, g, dim3(256), s, dst, dst_pitch, src, src_pitch, m);
+    launch_injection_rows(dst, dst_pitch, src, src_pitch, m, m, s);
 }
 
 void launch_injection_rows(double *dst, long dst_pitch, const double *src, long src_pitch,
                            long rows, long cols, hipStream_t s) {
     if (rows <= 0 || cols <= 0) return;
-    dim3 g(cdiv(cols, 256), (unsigned)rows);
+    dim3 g(cdiv(cols, 256), grid_y(rows));
     MGX_LAUNCH(k_injection_rows, g, dim3(256), s, dst, dst_pitch, src, src_pitch, rows, cols);
 }
 
@@ -1862,33 +1663,6 @@ void launch_gs_sweep(const double *uin, double *uout, const double *rhs, const d
             MGX_LAUNCH((k_gs_sweep<B, false>), g, dim3(B), s, uin, uout, rhs, v1, v2, (int)n,
                        pitch, R, c);
     }
-}
-
-template <int BLOCK, int K, int MODE>
-static int smooth_inst(const SmoothArgs &A, hipStream_t s) {
-    constexpr int W = 2 * (BLOCK - 2 * SmoothCfg<K, MODE>::H);
-    static int slots = 0;   // resident workgroups of this instantiation
-    if (!slots) {
-        int dev = 0, cus = 0, per = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_smooth<BLOCK, K, MODE>,
-                                                           BLOCK, 0);
-        slots = std::max(1, cus) * std::max(1, per);
-    }
-    const long n = A.n;
-    const int strips = (int)((n + 1 + W - 1) / W);
-    const long total = (long)strips * (A.rb - A.ra);
-    // at least ~64 rows per workgroup so the priming rows stay cheap; NORM
-    // partials are bounded by the partials buffer
-    long g = std::max<long>(1, std::min<long>(slots, total / 64));
-    g = std::min<long>(g, kNormBlocks);
-    const long upw = (total + g - 1) / g;
-    const unsigned grid = (unsigned)((total + upw - 1) / upw);
-    MGX_LAUNCH((k_smooth<BLOCK, K, MODE>), dim3(grid), dim3(BLOCK), s, A.uin, A.uout, A.rhs, A.v1,
-               A.v2, A.uc, A.pitchc, A.rhsc, A.partials, (int)n, A.pitch, strips, upw, A.c, A.ra,
-               A.rb, A.lo, A.hi);
-    return (int)grid;
 }
 
 long g_xfast = 1;   // unguarded interior march kernels (tuning key "xfast")
@@ -2005,31 +1779,6 @@ static int smooth_winst(const SmoothArgs &A, hipStream_t s) {
 }
 
 
-long g_xoverlap = 0;   // tuning key "xoverlap"
-void set_xoverlap(long v) { g_xoverlap = v; }
-long get_xoverlap() { return g_xoverlap; }
-
-// One non-blocking side stream + fork/join events per device (created on first use).
-struct SideStream {
-    hipStream_t s = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-};
-static SideStream *side_stream() {
-    static SideStream per_dev[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-    SideStream &ss = per_dev[dev];
-    if (!ss.s) {
-        if (hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess) {
-            ss = SideStream{};
-            return nullptr;
-        }
-    }
-    return &ss;
-}
-
 template <int WPB, int K, bool G>
 static int xsmooth_slots() {
     static int slots = 0;   // resident workgroups of this instantiation
@@ -2076,36 +1825,19 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
         lo = 0;
         hi = (int)n;
     }
-#ifdef MGX_PROBE_CLAMP
-    lo = hi = 2;   // experiment build only: every load from one row (L2-resident)
-#endif
     // inner: WPB pairs per workgroup, one workgroup per CU, long segments;
     // edge: one pair per workgroup (4 per CU) and short segments, so that its
     // ~44 K strip-rows at N=16384 (2 boundary strips + 71-row bands) take
     // about one warm-up + 44 rows per workgroup
     MarchRegions inner, edge, unused;
-    const bool split = g_xfast != 0;
+    // the unguarded kernel's division assumes d > 0 (div_diag<true>)
+    const bool split = g_xfast != 0 && A.c.dgs > 0;
     march_regions<WPB>(n, X::W, X::H, ra, rb, X::TOP, X::BOT, split, inner, unused);
     march_regions<1>(n, X::W, X::H, ra, rb, X::TOP, X::BOT, split, unused, edge);
     const int pm = xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, 64,
                                                  kNormBlocks / WPB / 2, s);
-    // xoverlap: the edge kernel on a side stream (forked after the inner
-    // launch, joined before the caller's next launch), so its workgroups take
-    // the CUs the inner kernel's last workgroups free.  Outputs are disjoint
-    // (strips / rows, partials ranges); inputs are read only.
-    hipStream_t se = s;
-    SideStream *ss = g_xoverlap && pm > 0 ? side_stream() : nullptr;
-    if (ss) {
-        (void)hipEventRecord(ss->fork, s);
-        (void)hipStreamWaitEvent(ss->s, ss->fork, 0);
-        se = ss->s;
-    }
     const int pe = xsmooth_launch<1, K, true>(A, edge, A.partials + pm, lo, hi, 32,
-                                              kNormBlocks / 2, se);
-    if (ss) {
-        (void)hipEventRecord(ss->join, ss->s);
-        (void)hipStreamWaitEvent(s, ss->join, 0);
-    }
+                                              kNormBlocks / 2, s);
     return pm + pe;
 }
 
@@ -2125,19 +1857,6 @@ int launch_xsmooth(const XArgs &A, int sweeps, hipStream_t s) {
                    blocks, A.norm_out, A.norm_sqrt ? 1 : 0);
     return blocks;
 }
-
-long g_march_kernel = -1;   // row march: 0 workgroup + LDS ring (k_smooth), 1 wave-private
-                            // k_wsmooth, 4 waves per workgroup, 2 the same, 1 wave
-
-static long march_kernel() {
-    if (g_march_kernel < 0) {
-        const char *e = getenv("MGX_MARCH_KERNEL");
-        g_march_kernel = e ? atol(e) : 1;
-    }
-    return g_march_kernel;
-}
-void set_march_kernel(long v) { g_march_kernel = v; }
-long get_march_kernel() { return march_kernel(); }
 
 long g_tile_max_n = -1;   // levels with n <= this use k_smooth_tile
 
@@ -2199,33 +1918,21 @@ static int smooth_tile_inst(const SmoothArgs &A, hipStream_t s) {
     return smooth_tile_rows<K, MODE, 16>(A, s);
 }
 
-long g_march_block = -1;   // workgroup width of the row march for n >= 4096
-
-static long march_block() {
-    if (g_march_block < 0) {
-        const char *e = getenv("MGX_MARCH_BLOCK");
-        g_march_block = e ? atol(e) : 256;
-    }
-    return g_march_block;
-}
-void set_march_block(long v) { g_march_block = v; }
-long get_march_block() { return march_block(); }
-
 template <int K, int MODE>
 static int smooth_block(const SmoothArgs &A, hipStream_t s) {
     // the row march needs >= ~32 rows per wave to amortise its priming rows;
     // a row block too small to give every resident wave that much (a
     // partitioned level on many GPUs) runs as LDS tiles instead
     bool tile = A.n <= tile_max_n();
-    if (!tile && march_kernel() == 1) {
+    if (!tile) {
         constexpr int W4 = WCfg<K, MODE>::W * 4;
         static int slots = 0;
         if (!slots) {
             int dev = 0, cus = 0, per = 0;
             (void)hipGetDevice(&dev);
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_wsmooth<4, K, MODE, false>, 256,
-                                                               0);
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_wsmooth<4, K, MODE, true>,
+                                                               256, 0);
             slots = std::max(1, cus) * std::max(1, per);
         }
         const long groups = (A.n + 1 + W4 - 1) / W4;
@@ -2235,13 +1942,9 @@ static int smooth_block(const SmoothArgs &A, hipStream_t s) {
         const int g = smooth_tile_inst<K, MODE>(A, s);
         if (g > 0) return g;
     }
-    if (A.n >= 4096) {
-        if (march_kernel() == 1) return smooth_winst<4, K, MODE>(A, s);
-        if (march_kernel() == 2) return smooth_winst<1, K, MODE>(A, s);
-        if (march_block() == 128) return smooth_inst<128, K, MODE>(A, s);
-        return smooth_inst<256, K, MODE>(A, s);
-    }
-    return smooth_inst<64, K, MODE>(A, s);
+    // the wave-private row march (also the fallback when a tile launch would
+    // need more norm partials than the buffer holds)
+    return smooth_winst<4, K, MODE>(A, s);
 }
 
 template <int K>
@@ -2268,13 +1971,6 @@ int launch_smooth(const SmoothArgs &A0, int sweeps, int mode, hipStream_t s) {
         A.hi = (int)A.n;
     }
     if (A.ra & 1) return -1;   // partitions start at even rows (parity, restriction)
-#ifdef MGX_PROBE_CLAMP
-    {   // experiment build only: every load from one row (L2-resident) -> the
-        // pass's compute + store time without the HBM read streams
-        A.lo = A.hi = 2;
-        A.uout = const_cast<double *>(A.uin);
-    }
-#endif
     int blocks = -1;
     switch (sweeps) {
         case 1: blocks = smooth_k<1>(A, mode, s); break;

@@ -64,6 +64,7 @@ int prof_flush(mgx_ctx *c) {
         int lvl = r.level < 0 ? 0 : (r.level > 63 ? 63 : r.level);
         c->sum_ms[r.kind][lvl] += ms;
         c->sum_bytes[r.kind][lvl] += r.bytes;
+        c->sum_cbytes[r.kind][lvl] += r.cbytes;
         c->count[r.kind][lvl] += 1;
         c->pool.push_back(r.e0);
         c->pool.push_back(r.e1);
@@ -133,8 +134,13 @@ int op_smooth(mgx_ctx *c, int l, int sweeps, bool prolong, bool restrict_, bool 
             }
             if (rs) bytes += 40.0 * L.M() + 24.0 * c->lv[l + 1].M();
             if (nm) bytes += 48.0 * L.M();
+            // compulsory: u (unless zero), rhs, v1, v2 read, u written, the
+            // coarse u read (prolong) / coarse rhs written (restrict)
+            const double cbytes = 8.0 * (((mode & mgx::kModeZero) ? 4.0 : 5.0) * L.M() +
+                                         ((pr ? 1 : 0) + (rs ? 1 : 0)) * c->lv[l + 1].M());
             int blocks = 0;
-            CHK(launch(c, kind, l, bytes, [&] { blocks = mgx::launch_smooth(A, k, mode, c->stream); }));
+            CHK(launch(c, kind, l, bytes, cbytes,
+                       [&] { blocks = mgx::launch_smooth(A, k, mode, c->stream); }));
             if (blocks < 0) return fail(MGX_E_ARG, "launch_smooth: unsupported sweeps/mode");
             L.cur = L.nxt();
             L.zero = false;
@@ -185,7 +191,7 @@ int read_norm(mgx_ctx *c, double *norm) {
 int op_residual_norm(mgx_ctx *c, int l, double *norm, double bytes_per_pt) {
     CHK(materialize(c, l));
     Level &L = c->lv[l];
-    CHK(launch(c, MGX_K_RESNORM, l, bytes_per_pt * L.M(), [&] {
+    CHK(launch(c, MGX_K_RESNORM, l, bytes_per_pt * L.M(), 32.0 * L.M(), [&] {
         mgx::launch_residual_norm(L.U(), L.rhs, L.v1, L.v2, L.n, L.pitch, L.coef, c->partials,
                                   c->dscal, c->stream);
     }));
@@ -196,7 +202,7 @@ int op_residual_norm(mgx_ctx *c, int l, double *norm, double bytes_per_pt) {
 int op_restrict(mgx_ctx *c, int l) {
     CHK(materialize(c, l));
     Level &F = c->lv[l], &C = c->lv[l + 1];
-    CHK(launch(c, MGX_K_RESTRICT, l, 40.0 * F.M() + 24.0 * C.M(), [&] {
+    CHK(launch(c, MGX_K_RESTRICT, l, 40.0 * F.M() + 24.0 * C.M(), 32.0 * F.M() + 8.0 * C.M(), [&] {
         mgx::launch_residual_restrict(F.U(), F.rhs, F.v1, F.v2, F.n, F.pitch, F.coef, C.rhs,
                                       C.pitch, c->stream);
     }));
@@ -209,7 +215,7 @@ int op_prolong_add(mgx_ctx *c, int l) {
     CHK(materialize(c, l));
     CHK(materialize(c, l + 1));
     Level &F = c->lv[l], &C = c->lv[l + 1];
-    CHK(launch(c, MGX_K_PROLONG, l, 32.0 * F.M() + 8.0 * C.M(), [&] {
+    CHK(launch(c, MGX_K_PROLONG, l, 32.0 * F.M() + 8.0 * C.M(), 16.0 * F.M() + 8.0 * C.M(), [&] {
         mgx::launch_prolong_add(F.U(), F.pitch, C.U(), C.pitch, C.n, c->stream);
     }));
     return MGX_OK;
@@ -220,7 +226,7 @@ int op_coarse(mgx_ctx *c, int l) {
     Level &L = c->lv[l];
     if (L.n <= mgx::kCoarseOneWgMaxN) {
         const bool z = L.zero;
-        CHK(launch(c, MGX_K_COARSE, l, 88.0 * L.M(), [&] {
+        CHK(launch(c, MGX_K_COARSE, l, 88.0 * L.M(), 40.0 * L.M(), [&] {
             mgx::launch_coarse_solve(L.U(), L.rhs, L.v1, L.v2, L.n, L.pitch, L.coef,
                                      c->opt.coarse_tol, c->opt.coarse_maxit, z, c->dscal + 2,
                                      c->stream);
@@ -288,8 +294,11 @@ static int op_cross(mgx_ctx *c, bool store_post) {
     // k) + k sweeps, residual+restriction (pre of cycle k+1), SURVEY 8d
     const double bytes = (32.0 + 40.0 * k + 48.0) * L.M() + 8.0 * Cl.M() +
                          (40.0 * k + 40.0) * L.M() + 24.0 * Cl.M();
+    // compulsory: u, rhs, v1, v2 and the coarse u read once; u_pre (+ u_post)
+    // and the coarse rhs written once
+    const double cbytes = 8.0 * ((store_post ? 6.0 : 5.0) * L.M() + 2.0 * Cl.M());
     int blocks = 0;
-    CHK(launch(c, MGX_K_XSMOOTH, 0, bytes,
+    CHK(launch(c, MGX_K_XSMOOTH, 0, bytes, cbytes,
                [&] { blocks = mgx::launch_xsmooth(A, k, c->stream); }));
     if (blocks < 0) return fail(MGX_E_ARG, "launch_xsmooth: unsupported sweeps");
     L.cur = P;
@@ -775,38 +784,47 @@ int mgx_profile_reset(mgx_ctx *c) {
     CHK(prof_flush(c));
     memset(c->sum_ms, 0, sizeof(c->sum_ms));
     memset(c->sum_bytes, 0, sizeof(c->sum_bytes));
+    memset(c->sum_cbytes, 0, sizeof(c->sum_cbytes));
     memset(c->count, 0, sizeof(c->count));
     for (int i = 0; i < dist_nsub(c); ++i) CHK(mgx_profile_reset(dist_sub(c, i)));
     return MGX_OK;
 }
 // Partitioned contexts: the replicated levels' launches (sub-contexts, level
 // numbers shifted by the first replicated level) are included.
-int mgx_profile_get(mgx_ctx *c, int kind, int level, long *launches, double *ms, double *bytes) {
+int mgx_profile_get_ex(mgx_ctx *c, int kind, int level, long *launches, double *ms,
+                       double *bytes, double *cbytes) {
     if (!c || kind < 0 || kind >= MGX_K_COUNT || level >= 64)
         return fail(MGX_E_ARG, "mgx_profile_get: bad args");
     CHK(prof_flush(c));
     long n = 0;
-    double t = 0, b = 0;
+    double t = 0, b = 0, cb = 0;
     for (int l = 0; l < 64; ++l) {
         if (level >= 0 && l != level) continue;
         n += c->count[kind][l];
         t += c->sum_ms[kind][l];
         b += c->sum_bytes[kind][l];
+        cb += c->sum_cbytes[kind][l];
     }
     const int la = dist_la(c);
     for (int i = 0; i < dist_nsub(c); ++i) {
         if (level >= 0 && level < la) break;
         long sn = 0;
-        double st = 0, sb = 0;
-        CHK(mgx_profile_get(dist_sub(c, i), kind, level < 0 ? -1 : level - la, &sn, &st, &sb));
+        double st = 0, sb = 0, scb = 0;
+        CHK(mgx_profile_get_ex(dist_sub(c, i), kind, level < 0 ? -1 : level - la, &sn, &st, &sb,
+                               &scb));
         n += sn;
         t += st;
         b += sb;
+        cb += scb;
     }
     if (launches) *launches = n;
     if (ms) *ms = t;
     if (bytes) *bytes = b;
+    if (cbytes) *cbytes = cb;
     return MGX_OK;
+}
+int mgx_profile_get(mgx_ctx *c, int kind, int level, long *launches, double *ms, double *bytes) {
+    return mgx_profile_get_ex(c, kind, level, launches, ms, bytes, nullptr);
 }
 
 // ---- timestepper (multigrid.cpp:124-186)
@@ -910,19 +928,9 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgx::set_tile_max_n(value);
         return MGX_OK;
     }
-    if (!strcmp(key, "march_block")) {
-        if (value != 128 && value != 256) return fail(MGX_E_ARG, "march_block must be 128 or 256");
-        mgx::set_march_block(value);
-        return MGX_OK;
-    }
     if (!strcmp(key, "cross_cycle")) {
         if (value != 0 && value != 1) return fail(MGX_E_ARG, "cross_cycle must be 0 or 1");
         mgxi::g_cross_cycle = value;
-        return MGX_OK;
-    }
-    if (!strcmp(key, "march_kernel")) {
-        if (value < 0 || value > 2) return fail(MGX_E_ARG, "march_kernel must be 0, 1 or 2");
-        mgx::set_march_kernel(value);
         return MGX_OK;
     }
     if (!strcmp(key, "dist_min_rows")) {
@@ -955,11 +963,6 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgx::set_march_min_rows(value);
         return MGX_OK;
     }
-    if (!strcmp(key, "xoverlap")) {
-        if (value != 0 && value != 1) return fail(MGX_E_ARG, "xoverlap must be 0 or 1");
-        mgx::set_xoverlap(value);
-        return MGX_OK;
-    }
     if (!strcmp(key, "coarse_lds")) {
         if (value != 0 && value != 1) return fail(MGX_E_ARG, "coarse_lds must be 0 or 1");
         mgx::set_coarse_lds(value);
@@ -973,17 +976,9 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
         *value = mgx::get_tile_max_n();
         return MGX_OK;
     }
-    if (!strcmp(key, "march_block")) {
-        *value = mgx::get_march_block();
-        return MGX_OK;
-    }
     if (!strcmp(key, "cross_cycle")) {
         mgxi::cross_cycle_on();
         *value = mgxi::g_cross_cycle;
-        return MGX_OK;
-    }
-    if (!strcmp(key, "march_kernel")) {
-        *value = mgx::get_march_kernel();
         return MGX_OK;
     }
     if (!strcmp(key, "dist_min_rows")) {
@@ -1008,10 +1003,6 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "march_min_rows")) {
         *value = mgx::get_march_min_rows();
-        return MGX_OK;
-    }
-    if (!strcmp(key, "xoverlap")) {
-        *value = mgx::get_xoverlap();
         return MGX_OK;
     }
     if (!strcmp(key, "coarse_lds")) {

@@ -57,3 +57,21 @@ def partition(n: int, maxlvl: int, world: int, rank: int, level: int):
     check(lib().mgx_partition(n, maxlvl, world, rank, level, C.byref(ra), C.byref(rb),
                               C.byref(la)))
     return ra.value, rb.value, la.value
+
+
+def exchange_plan(n: int, maxlvl: int, world: int, rank: int, level: int):
+    """Ghost-row transfers of `rank` on `level` as libmgx executes them (both
+    transports): [(peer, send_row, send_rows, recv_row, recv_rows), ...]."""
+    cnt = C.c_int()
+    buf = (C.c_int * 10)()
+    check(lib().mgx_exchange_plan(n, maxlvl, world, rank, level, C.byref(cnt), buf, 2))
+    return [tuple(buf[5 * i:5 * i + 5]) for i in range(cnt.value)]
+
+
+def gather_plan(n: int, maxlvl: int, world: int, rank: int):
+    """-> (level, row0, rows): rows `rank` contributes to the all-gather into the
+    first replicated level."""
+    lv, r0, rows = C.c_int(), C.c_int(), C.c_int()
+    check(lib().mgx_gather_plan(n, maxlvl, world, rank, C.byref(lv), C.byref(r0),
+                                C.byref(rows)))
+    return lv.value, r0.value, rows.value

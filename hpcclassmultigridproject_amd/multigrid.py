@@ -225,3 +225,10 @@ class Multigrid:
         n, ms, b = C.c_long(), C.c_double(), C.c_double()
         check(lib().mgx_profile_get(self._h, kind, level, C.byref(n), C.byref(ms), C.byref(b)))
         return n.value, ms.value, b.value
+
+    def profile_get_ex(self, kind, level=-1):
+        """(launches, device ms, canonical algorithmic bytes, compulsory bytes)"""
+        n, ms, b, cb = C.c_long(), C.c_double(), C.c_double(), C.c_double()
+        check(lib().mgx_profile_get_ex(self._h, kind, level, C.byref(n), C.byref(ms),
+                                       C.byref(b), C.byref(cb)))
+        return n.value, ms.value, b.value, cb.value

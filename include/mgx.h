@@ -32,6 +32,7 @@ extern "C" {
 #define MGX_E_HIP 2     /* a HIP runtime call failed */
 #define MGX_E_RCCL 3    /* an RCCL call failed */
 #define MGX_E_NOCONV 4  /* mg_outer hit its cycle cap (reported, not fatal) */
+#define MGX_E_INTERNAL 5 /* an internal consistency check failed (a bug) */
 
 const char *mgx_last_error(void);
 int mgx_version(void);
@@ -159,15 +160,12 @@ int mgx_synchronize(mgx_ctx *ctx);
 
 /* Process-wide tuning knobs.  "tile_max_n": levels with n <= value run the
  * fused smoothing pass as 2-D LDS tiles instead of the row march (default 2048;
- * env MGX_TILE_MAX_N).  "march_block": lanes per workgroup of the row march on
- * levels with n >= 4096, 128 or 256 (default 256; env MGX_MARCH_BLOCK).
+ * env MGX_TILE_MAX_N).
  * "cross_cycle": 1 (default) fuses, inside mg_outer / run_cycles / step, the
  * finest level's post-smoothing of each V-cycle with the pre-smoothing of
  * the next into one HBM pass (levels with n >= 4096, V-cycles, nsmooth 2 or
  * 3; bitwise the same results); after such a cycle the coarse levels hold
  * the next cycle's restricted rhs, not the last correction.  0 = off.
- * "march_kernel": row march on levels with n >= 4096: 1 wave-private
- * registers + DPP (default), 0 workgroup with an LDS ring (env MGX_MARCH_KERNEL).
  * "dist_min_rows": partitioned solvers replicate every level whose row blocks
  * would be shorter than this (default 256, even, >= 16); read at creation.
  * "xfast": 1 (default) runs the cross-cycle pass as an unguarded kernel over
@@ -180,8 +178,7 @@ int mgx_synchronize(mgx_ctx *ctx);
  * (env MGX_MARCH_ORDER).  "tile_xcd": 1 (default) deals the LDS tiles
  * XCD-contiguous.  "tile32_min_n": K=3 tile passes on levels n >= value use
  * 32-row tiles (default 2048).  "march_min_rows": fewest rows per workgroup
- * of a wave-march launch (default 64, >= 8).  "xoverlap": 1 runs the cross
- * pass's edge kernel on a side stream next to the interior kernel (default 0).
+ * of a wave-march launch (default 64, >= 8).
  * "coarse_lds": 1 (default) solves coarsest levels n <= 64 with the fields
  * in LDS, 0 = through L2 (bitwise the same).
  * None of them changes a result bit. */
@@ -207,6 +204,11 @@ int mgx_profile_reset(mgx_ctx *ctx);
  * device milliseconds, summed algorithmic bytes (SURVEY 8d byte model). */
 int mgx_profile_get(mgx_ctx *ctx, int kind, int level, long *launches, double *ms,
                     double *bytes);
+/* The same plus the compulsory bytes of those launches: every array a launch
+ * reads or writes counted once (the traffic floor of a fused pass, and the
+ * roofline denominator bench.py reports). */
+int mgx_profile_get_ex(mgx_ctx *ctx, int kind, int level, long *launches, double *ms,
+                       double *bytes, double *cbytes);
 
 /* ---- Row-partitioned multi-GPU solver ---------------------------
  * The finest levels are split into contiguous row blocks, one per rank, with
@@ -239,6 +241,18 @@ int mgx_create_local_dist(mgx_ctx **out, long n, int maxlvl, double dt, double n
  * the first replicated level (levels >= it are whole on every rank). */
 int mgx_partition(long n, int maxlvl, int world, int rank, int level, int *ra, int *rb,
                   int *replicated_level);
+/* Host-only: the ghost-row exchange plan of `rank` on `level` (both transports
+ * execute it).  *count entries of 5 ints: peer, send_row, send_rows, recv_row,
+ * recv_rows (global rows of the level: send rows [send_row, +send_rows) to
+ * peer, receive rows [recv_row, +recv_rows) from it); 0 entries on replicated
+ * levels or world 1.  cap = room in xfers (entries). */
+int mgx_exchange_plan(long n, int maxlvl, int world, int rank, int level, int *count,
+                      int *xfers, int cap);
+/* Host-only: the all-gather into the first replicated level *level: `rank`
+ * contributes rows [*row0, *row0 + *rows) of its restricted rhs (in place,
+ * rank-major, equal counts). */
+int mgx_gather_plan(long n, int maxlvl, int world, int rank, int *level, int *row0,
+                    int *rows);
 /* Allocated rows [*lo, *hi] (owned + ghosts) of the finest level of local part
  * `part` (0 on an RCCL rank; 0..world-1 for mgx_create_local_dist). */
 int mgx_dist_rows(mgx_ctx *ctx, int part, int *lo, int *hi);

@@ -305,3 +305,111 @@ void or_init_problem(double *u0, double *v1, double *v2, long N) {
         u0[i * w] = 0.0;
     }
 }
+
+/* ---------------------------------------------------------------- row slabs
+ * The gs.h ops on a window of rows: the arrays hold global rows [r0, r0+nr)
+ * of an (n+1)^2 field (row-major, width n+1), so a test can check the device
+ * ops at sizes where the whole field does not fit the host (N = 65536: 4.3e9
+ * points per array).  Same expressions and term order as the
+ * whole-field functions above; only points whose stencil lies inside the
+ * window are updated: a slab result is the whole-field result on rows
+ * [r0+1, r0+nr-2] (residual / compute_rhs) and [r0+2, r0+nr-3] (gauss_seidel,
+ * whose black half reads red values one row further out). */
+static void slab_rows(long n, long r0, long nr, long *i0, long *i1) {
+    *i0 = r0 + 1 > 1 ? r0 + 1 : 1;
+    *i1 = r0 + nr - 1 < n ? r0 + nr - 1 : n; /* exclusive */
+}
+
+/* gs.cpp:109-189 on a slab */
+void or_gauss_seidel_slab(double *u, const double *rhs, long n, long r0, long nr,
+                          const double *v1, const double *v2, double k, double nu, double h) {
+    const double rr = coef_r(h, k);
+    const long w = n + 1;
+    long i0, i1;
+    slab_rows(n, r0, nr, &i0, &i1);
+    for (int colour = 0; colour < 2; colour++) {
+#pragma omp parallel for schedule(static) if (g_threads > 1) num_threads(g_threads)
+        for (long i = i0; i < i1; i++) {
+            const long j0 = (colour == 0) ? (2 - (i & 1)) : (1 + (i & 1));
+            for (long j = j0; j < n; j += 2) {
+                const long p = (i - r0) * w + j;
+                const double aa = coef_a(v2[p], nu, h, rr);
+                const double bb = coef_b(v2[p], nu, h, rr);
+                const double cc = coef_a(v1[p], nu, h, rr);
+                const double dd = coef_b(v1[p], nu, h, rr);
+                u[p] = (rhs[p] - cc * u[p - w] - aa * u[p - 1] - dd * u[p + w] -
+                        bb * u[p + 1]) /
+                       (1.0 - 4.0 * rr * nu);
+            }
+        }
+    }
+}
+
+/* gs.cpp:55-83 on a slab */
+void or_residual_slab(double *res, const double *u, const double *rhs, long n, long r0,
+                      long nr, const double *v1, const double *v2, double k, double nu,
+                      double h) {
+    const double rr = coef_r(h, k);
+    const long w = n + 1;
+    long i0, i1;
+    slab_rows(n, r0, nr, &i0, &i1);
+#pragma omp parallel for schedule(static) if (g_threads > 1) num_threads(g_threads)
+    for (long i = i0; i < i1; i++) {
+        for (long j = 1; j < n; j++) {
+            const long p = (i - r0) * w + j;
+            const double aa = coef_a(v2[p], nu, h, rr);
+            const double bb = coef_b(v2[p], nu, h, rr);
+            const double cc = coef_a(v1[p], nu, h, rr);
+            const double dd = coef_b(v1[p], nu, h, rr);
+            res[p] = rhs[p] - ((1.0 - 4.0 * rr * nu) * u[p] + cc * u[p - w] +
+                               aa * u[p - 1] + dd * u[p + w] + bb * u[p + 1]);
+        }
+    }
+}
+
+/* gs.cpp:24-53 on a slab */
+void or_compute_rhs_slab(double *rhs, const double *u, long n, long r0, long nr,
+                         const double *v1, const double *v2, double k, double nu, double h) {
+    const double rr = coef_r(h, k);
+    const long w = n + 1;
+    long i0, i1;
+    slab_rows(n, r0, nr, &i0, &i1);
+#pragma omp parallel for schedule(static) if (g_threads > 1) num_threads(g_threads)
+    for (long i = i0; i < i1; i++) {
+        for (long j = 1; j < n; j++) {
+            const long p = (i - r0) * w + j;
+            const double aa = coef_a(v2[p], nu, h, rr);
+            const double bb = coef_b(v2[p], nu, h, rr);
+            const double cc = coef_a(v1[p], nu, h, rr);
+            const double dd = coef_b(v1[p], nu, h, rr);
+            rhs[p] = (1.0 + 4.0 * rr * nu) * u[p] - cc * u[p - w] - aa * u[p - 1] -
+                     dd * u[p + w] - bb * u[p + 1];
+        }
+    }
+}
+
+/* gs.cpp:228-266 for fine rows [2 c0, 2 (c0 + cn - 1)] (clipped to 2n) from
+ * coarse rows [c0, c0 + cn): up holds those fine rows (width 2n+1).  The
+ * interior formulas (gs.cpp:238-241) and the border ones (gs.cpp:251-265) are
+ * the same expressions at i = n or j = n, evaluated per fine point here. */
+void or_prolongation_slab(double *up, const double *u, long n, long c0, long cn) {
+    const long w = n + 1, W = 2 * n + 1;
+    long I1 = 2 * (c0 + cn - 1);
+    if (I1 > 2 * n) I1 = 2 * n;
+#pragma omp parallel for schedule(static) if (g_threads > 1) num_threads(g_threads)
+    for (long I = 2 * c0; I <= I1; I++) {
+        const long i = I >> 1;
+        const double *r0 = u + (i - c0) * w;
+        for (long J = 0; J < W; J++) {
+            const long j = J >> 1;
+            double v;
+            if (!(I & 1))
+                v = (J & 1) ? (r0[j] + r0[j + 1]) / 2 : r0[j];
+            else if (!(J & 1))
+                v = (r0[j] + r0[w + j]) / 2;
+            else
+                v = (r0[j] + r0[w + j] + r0[j + 1] + r0[w + j + 1]) / 4;
+            up[(I - 2 * c0) * W + J] = v;
+        }
+    }
+}

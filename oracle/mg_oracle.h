@@ -36,6 +36,16 @@ void or_gauss_seidel(double *u, const double *rhs, long n, const double *v1,
 void or_prolongation(double *up, const double *u, long n);
 /* gs.cpp:268-292 */
 void or_restriction(double *u, const double *up, long n);
+/* Row-slab forms (arrays hold global rows [r0, r0+nr) of an (n+1)^2 field),
+ * for checking the device ops at N where a field does not fit the host. */
+void or_gauss_seidel_slab(double *u, const double *rhs, long n, long r0, long nr,
+                          const double *v1, const double *v2, double k, double nu, double h);
+void or_residual_slab(double *res, const double *u, const double *rhs, long n, long r0,
+                      long nr, const double *v1, const double *v2, double k, double nu,
+                      double h);
+void or_compute_rhs_slab(double *rhs, const double *u, long n, long r0, long nr,
+                         const double *v1, const double *v2, double k, double nu, double h);
+void or_prolongation_slab(double *up, const double *u, long n, long c0, long cn);
 
 /* multigrid.cpp:17-92.  nsmooth = NITER (multigrid.cpp:41, 3 in the reference).
  * Returns the total number of coarsest-level GS iterations performed. */

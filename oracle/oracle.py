@@ -5,7 +5,8 @@ module.  It wraps
   * oracle/liboracle.so      -- the C restatement of the reference (mg_oracle.c)
   * oracle/_ref/libmgref.so  -- the unmodified reference sources, compiled here
                                 (optional: only present where /root/reference
-                                was available at build time)
+                                was available at build time); libmgref_o3.so
+                                is the same sources at -O3 (CPU baseline only)
 All arrays are float64 numpy arrays in the reference's row-major (n+1)^2 layout.
 """
 from __future__ import annotations
@@ -19,6 +20,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 REF_PATH = os.path.join(HERE, "_ref", "libmgref.so")
 REF_NU2_PATH = os.path.join(HERE, "_ref", "libmgref_nu2.so")   # NITER = 2 (config 2)
+REF_O3_PATH = os.path.join(HERE, "_ref", "libmgref_o3.so")     # -O3 -march=x86-64-v3
 
 _dp = C.POINTER(C.c_double)
 
@@ -114,6 +116,43 @@ def restriction(up, n):
     return u
 
 
+def gauss_seidel_slab(u, rhs, n, r0, v1, v2, k, nu, h):
+    """gauss_seidel on rows [r0, r0 + rows) held in u (in place); exact on rows
+    [r0 + 2, r0 + rows - 3]."""
+    nr = u.size // (n + 1)
+    lib().or_gauss_seidel_slab(_p(u), _p(rhs), LNG(n), LNG(r0), LNG(nr), _p(v1), _p(v2),
+                               D(k), D(nu), D(h))
+    return u
+
+
+def residual_slab(u, rhs, n, r0, v1, v2, k, nu, h):
+    """residual on a row slab (zeros where not computed); exact on rows
+    [r0 + 1, r0 + rows - 2]."""
+    res = np.zeros_like(u)
+    nr = u.size // (n + 1)
+    lib().or_residual_slab(_p(res), _p(u), _p(rhs), LNG(n), LNG(r0), LNG(nr), _p(v1),
+                           _p(v2), D(k), D(nu), D(h))
+    return res
+
+
+def compute_rhs_slab(u, n, r0, v1, v2, k, nu, h):
+    rhs = np.zeros_like(u)
+    nr = u.size // (n + 1)
+    lib().or_compute_rhs_slab(_p(rhs), _p(u), LNG(n), LNG(r0), LNG(nr), _p(v1), _p(v2),
+                              D(k), D(nu), D(h))
+    return rhs
+
+
+def prolongation_slab(u, n, c0):
+    """Fine rows [2 c0, 2 (c0 + rows - 1)] (clipped to 2n) of prolongation(u)
+    from the coarse rows [c0, c0 + rows) held in u."""
+    cn = u.size // (n + 1)
+    I1 = min(2 * (c0 + cn - 1), 2 * n)
+    up = np.zeros((I1 - 2 * c0 + 1) * (2 * n + 1), dtype=np.float64)
+    lib().or_prolongation_slab(_p(up), _p(u), LNG(n), LNG(c0), LNG(cn))
+    return up
+
+
 def init_problem(N):
     cnt = (N + 1) ** 2
     u0, v1, v2 = (np.empty(cnt) for _ in range(3))
@@ -200,8 +239,26 @@ def ref_op(name, *args):
     return getattr(ref(), name)(*args)
 
 
-def ref_time_vcycles(n, maxlvl, nu, cycles, nthreads):
+_ref_o3 = None
+
+
+def ref_o3_available() -> bool:
+    return os.path.exists(REF_O3_PATH)
+
+
+def ref_o3():
+    """The unmodified reference sources built -O3 (timing only, never a checker)."""
+    global _ref_o3
+    if _ref_o3 is None:
+        _ref_o3 = _load(REF_O3_PATH)
+        _ref_o3.ref_time_vcycles.restype = C.c_double
+    return _ref_o3
+
+
+def ref_time_vcycles(n, maxlvl, nu, cycles, nthreads, opt="O0"):
+    """Seconds for `cycles` reference V-cycles (+ residual/norm) at size n on
+    `nthreads` OpenMP threads; opt "O0" = the reference Makefile flags, "O3"."""
     setup, res = D(), D()
-    t = ref().ref_time_vcycles(C.c_int(n), C.c_int(maxlvl), D(nu), C.c_int(cycles),
+    t = (ref_o3() if opt == "O3" else ref()).ref_time_vcycles(C.c_int(n), C.c_int(maxlvl), D(nu), C.c_int(cycles),
                                C.c_int(nthreads), C.byref(setup), C.byref(res))
     return t, setup.value, res.value

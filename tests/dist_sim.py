@@ -8,8 +8,12 @@ shows up as NaN in its owned rows.  The stencil arithmetic is the oracle's
 (oracle/mg_oracle.c, the reference's term order), the data movement is what
 dist.hip does, over torch.distributed (gloo): ghost rows from rank +-1
 (isend/irecv), all-gather of the restricted rhs into the first replicated
-level, all-reduce of the residual's sum of squares.  The partition plan comes
-from libmgx's own mgx_partition.
+level, all-reduce of the residual's sum of squares.  The partition, the
+ghost-row exchange plan and the all-gather rows all come from libmgx itself
+(mgx_partition, mgx_exchange_plan, mgx_gather_plan: the entries its RCCL
+transport posts as ncclSend/ncclRecv and ncclAllGather), so the processes
+here exchange exactly the rows, offsets and counts the RCCL ranks do; a rank's
+allocated rows are what that plan receives, everything else is NaN.
 
 Mirrors: dist.hip dist_level (pre pass + restrict, recurse / gather, post
 pass + prolong), multigrid.cpp:17-92 for the replicated levels.
@@ -24,15 +28,18 @@ import torch.distributed as dist
 
 from oracle import oracle as O
 
-K_GHOST = 8         # dist.hip kGhost
-K_GHOST_FINE = 16   # dist.hip kGhostFine (level 0: the cross-cycle pass)
+K_GHOST = 8         # dist.hip kGhost (the fewest ghost rows a block may hold)
 
 
 class Block:
-    def __init__(self, n, ra, rb, ghost=K_GHOST):
-        self.n, self.ra, self.rb = n, ra, rb
-        self.lo = max(0, ra - ghost)
-        self.hi = min(n, rb - 1 + ghost)
+    def __init__(self, n, ra, rb, xfers=()):
+        """Owned rows [ra, rb); allocated rows = owned + what `xfers` (the
+        library's exchange plan for this rank) receives."""
+        self.n, self.ra, self.rb, self.xfers = n, ra, rb, list(xfers)
+        self.lo, self.hi = ra, rb - 1
+        for peer, s0, sn, r0, rn in self.xfers:
+            assert r0 + rn <= ra or r0 >= rb, "plan receives into owned rows"
+            self.lo, self.hi = min(self.lo, r0), max(self.hi, r0 + rn - 1)
 
     def rows(self, a):
         return a.reshape(self.n + 1, self.n + 1)
@@ -44,21 +51,15 @@ class Block:
 
 
 def exchange(blk, a, rank, world):
-    """Ghost rows [lo, ra) from rank-1 and [rb, hi] from rank+1 (dist.hip exchange)."""
+    """The library's exchange plan for this rank and level, posted as gloo
+    isend/irecv pairs (dist.hip exchange_rows: ncclSend/ncclRecv)."""
     m = blk.rows(a)
     reqs, recv = [], []
-    if rank > 0:
-        g = blk.ra - blk.lo
-        reqs.append(dist.isend(torch.from_numpy(m[blk.ra:blk.ra + g].copy()), rank - 1))
-        buf = torch.empty((g, blk.n + 1), dtype=torch.float64)
-        reqs.append(dist.irecv(buf, rank - 1))
-        recv.append((blk.lo, buf))
-    if rank < world - 1:
-        g = blk.hi - blk.rb + 1
-        reqs.append(dist.isend(torch.from_numpy(m[blk.rb - g:blk.rb].copy()), rank + 1))
-        buf = torch.empty((g, blk.n + 1), dtype=torch.float64)
-        reqs.append(dist.irecv(buf, rank + 1))
-        recv.append((blk.rb, buf))
+    for peer, s0, sn, r0, rn in blk.xfers:
+        reqs.append(dist.isend(torch.from_numpy(m[s0:s0 + sn].copy()), peer))
+        buf = torch.empty((rn, blk.n + 1), dtype=torch.float64)
+        reqs.append(dist.irecv(buf, peer))
+        recv.append((r0, buf))
     for r in reqs:
         r.wait()
     for r0, buf in recv:
@@ -66,13 +67,14 @@ def exchange(blk, a, rank, world):
 
 
 class PartitionedVCycle:
-    def __init__(self, rank, world, N, L, tower, dt, nu, nsmooth, plan):
-        """plan(level) -> (ra, rb, la): mgx_partition for this rank."""
+    def __init__(self, rank, world, N, L, tower, dt, nu, nsmooth, plan, xplan, gplan):
+        """plan(level) -> (ra, rb, la): mgx_partition for this rank;
+        xplan(level) -> mgx_exchange_plan entries; gplan() -> mgx_gather_plan."""
         self.rank, self.world, self.N, self.L = rank, world, N, L
         self.dt, self.nu, self.nsmooth = dt, nu, nsmooth
         self.la = plan(0)[2]
-        self.blk = [Block(N >> l, *plan(l)[:2], K_GHOST_FINE if l == 0 else K_GHOST)
-                    for l in range(self.la)]
+        self.gplan = gplan
+        self.blk = [Block(N >> l, *plan(l)[:2], xplan(l)) for l in range(self.la)]
         self.spec = False   # cross-cycle mode: next cycle's pre-smoothing already done
         self.v1 = [tower.level("v1", l) for l in range(L)]
         self.v2 = [tower.level("v2", l) for l in range(L)]
@@ -155,14 +157,16 @@ class PartitionedVCycle:
         return None
 
     def _gather_rhs(self, l):
+        """dist.hip gather_rhs: the in-place all-gather of mgx_gather_plan's rows."""
         n = self.N >> l
-        q = n // self.world
+        la, r0, q = self.gplan()
+        assert la == l
         m = self.rhs[l].reshape(n + 1, n + 1)
-        mine = torch.from_numpy(m[self.rank * q:(self.rank + 1) * q].copy())
+        mine = torch.from_numpy(m[r0:r0 + q].copy())
         parts = [torch.empty_like(mine) for _ in range(self.world)]
         dist.all_gather(parts, mine)
         for r, t in enumerate(parts):
-            m[r * q:(r + 1) * q] = t.numpy()
+            m[r * q:(r + 1) * q] = t.numpy()   # rank-major (ncclAllGather in place)
 
     def _restrict_owned(self, l):
         """Residual of level l restricted into the owned rows of rhs[l+1]."""

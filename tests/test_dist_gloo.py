@@ -3,8 +3,9 @@
 * the unique-id broadcast that bootstraps libmgx's RCCL communicator;
 * the partition plan from libmgx (mgx_partition) as every rank sees it:
   blocks tile each level, start at even rows, hold >= the ghost width;
-* the partitioned V-cycle's data movement (tests/dist_sim.py: ghost
-  exchanges over gloo send/recv, all-gather into the replicated levels,
+* the partitioned V-cycle's data movement (tests/dist_sim.py: libmgx's own
+  exchange plan -- the ncclSend/ncclRecv entries its RCCL transport posts --
+  executed as gloo send/recv between the processes, libmgx's all-gather rows,
   norm all-reduce) with the oracle's stencils and NaN-poisoned non-local
   rows: each rank's owned rows after two V-cycles are BITWISE the
   single-process oracle's, and the all-reduced norm matches to 1e-12;
@@ -55,7 +56,9 @@ def _worker(rank, world, port, N, L, nsmooth, min_rows, q, cross=False):
         dt = 1.0 / N / 10
         tower = O.Tower(u0, v1, v2, N, L)
         sim = PartitionedVCycle(rank, world, N, L, tower, dt, NU, nsmooth,
-                                lambda l: mgd.partition(N, L, world, rank, l))
+                                lambda l: mgd.partition(N, L, world, rank, l),
+                                lambda l: mgd.exchange_plan(N, L, world, rank, l),
+                                lambda: mgd.gather_plan(N, L, world, rank))
         sim.u[0][:] = u0
         sim.rhs[0] = O.compute_rhs(u0, N, v1, v2, dt, NU, 1.0 / N)
         ncyc = 3 if cross else 2

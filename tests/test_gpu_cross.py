@@ -141,18 +141,17 @@ def knobs():
 @pytest.mark.parametrize("N,L,G", [(8192, 5, 1), (4096, 6, 4)], ids=["N8192", "N4096_G4"])
 def test_work_order_does_not_change_results(N, L, G, cross, knobs):
     """march_order (band-major rows, XCD-contiguous workgroups), tile_xcd /
-    tile32_min_n (tile order and 32-row tiles) and xoverlap (the cross pass's
-    edge kernel on a side stream) only reorder the work: u
+    tile32_min_n (tile order and 32-row tiles) only reorder the work: u
     bitwise, norms to the summation-order tolerance, on one GPU and on row
     blocks."""
     cross(1)
     kw = dict(local_parts=G) if G > 1 else {}
-    knobs(march_order=0, tile_xcd=0, tile32_min_n=1 << 30, xoverlap=0)
+    knobs(march_order=0, tile_xcd=0, tile32_min_n=1 << 30)
     u_ref, n_ref = _cycles_plain(N, L, 3, **kw)
-    for mo, tx, t32, xo in ((1, 0, 1 << 30, 0), (2, 1, 0, 1), (3, 1, 1024, 1)):
-        knobs(march_order=mo, tile_xcd=tx, tile32_min_n=t32, xoverlap=xo)
+    for mo, tx, t32 in ((1, 0, 1 << 30), (2, 1, 0), (3, 1, 1024)):
+        knobs(march_order=mo, tile_xcd=tx, tile32_min_n=t32)
         u, n = _cycles_plain(N, L, 3, **kw)
-        assert np.array_equal(u, u_ref), (mo, tx, t32, xo)
+        assert np.array_equal(u, u_ref), (mo, tx, t32)
         np.testing.assert_allclose(n, n_ref, rtol=NORM_RTOL)
 
 
@@ -170,3 +169,30 @@ def test_coarse_solve_in_lds_equals_l2_version(N, L, knobs):
             out.append((mg.download(), cyc, mg.coarse_iterations(), mg.residual_norm(0)))
     (ua, ca, ia, ra), (ub, cb, ib, rb) = out
     assert np.array_equal(ua, ub) and ca == cb and ia == ib and ra == rb
+
+
+def test_negative_diagonal_routes_to_general_division(cross, oracle_mod):
+    """nu > 0 large enough that the finest level's diagonal 1-4*rr*nu is
+    negative: the unguarded cross kernel's division form assumes d > 0, so the
+    launcher must run the level through the guarded kernel (general form, zero
+    signs included).  Two cycles bitwise vs the unfused schedule and the
+    checker (N=4096: rr = 204.8, nu = 0.002 -> d = -0.6384 on level 0)."""
+    N, L, nu = 4096, 3, 0.002
+    dt = 1.0 / N / 10
+    u0, v1, v2 = init_problem(N)
+    out = []
+    for on in (0, 1):
+        cross(on)
+        with Multigrid(N, L, dt, nu) as mg:
+            mg.upload(u0, v1, v2)
+            mg.rhs()
+            mg.run_cycles(2)
+            out.append(mg.download())
+    assert np.array_equal(out[0], out[1])
+    O = oracle_mod
+    O.set_threads(8)
+    t = O.Tower(u0, v1, v2, N, L)
+    O.compute_rhs(t.ufine, N, v1, v2, dt, nu, 1.0 / N, rhs=t.rhsfine)
+    for _ in range(2):
+        t.mg_inner(dt, nu)
+    assert np.array_equal(out[1], t.ufine)

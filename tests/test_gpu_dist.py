@@ -256,3 +256,44 @@ def test_row_block_upload_refuses_reference_tower():
         blk = init_problem_rows(1024, lo, hi + 1)
         with pytest.raises(MGXError):
             mg.upload_rows([blk, blk])
+
+
+# ---- config C4: N=16384 row-partitioned (virtual ranks on the one-GPU box;
+# the same partition plan and exchange plan the RCCL ranks execute)
+@pytest.mark.slow
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_C4_vcycle_partitioned_N16384(golden_summary, G):
+    """Headline size on G row blocks (levels 0..la-1 partitioned, the rest
+    replicated): one V-cycle bitwise = the reference's sha256."""
+    s = golden_summary["vcycle"]["N16384_L9"]
+    N, L = 16384, 9
+    u0, v1, v2 = init_problem(N, nthreads=16)
+    with Multigrid(N, L, 1.0 / N / 10, NU, local_parts=G) as mg:
+        assert mg.dist_info()[0] == G and mg.dist_info()[2] >= 3
+        mg.upload(u0, v1, v2)
+        del v1, v2
+        mg.rhs()
+        mg.mg_inner()
+        u = mg.download(u0)
+    assert hashlib.sha256(u.tobytes()).hexdigest() == s["sha256"]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_C4_two_timesteps_partitioned_N16384(golden_summary, G):
+    """Two Crank-Nicolson steps (rhs + mg_outer with the cross-cycle pass on
+    row blocks): cycles [3, 3] and the reference's sha256."""
+    s = golden_summary["steps"]["N16384_L9_2steps"]
+    N, L = 16384, 9
+    u0, v1, v2 = init_problem(N, nthreads=16)
+    with Multigrid(N, L, 1.0 / N / 10, NU, local_parts=G) as mg:
+        mg.upload(u0, v1, v2)
+        del v1, v2
+        mg.profile(True, finest_only=True)
+        cyc = [mg.step(1e-6) for _ in range(2)]
+        xs = mg.profile_get(_lib.K_XSMOOTH)[0]
+        mg.profile(False)
+        u = mg.download(u0)
+    assert cyc == [3, 3]
+    assert xs == 6 * G   # the cross-cycle pass ran on every block, every cycle
+    assert hashlib.sha256(u.tobytes()).hexdigest() == s["sha256"]

@@ -1,0 +1,162 @@
+"""Config C5 scale on one GPU: N = 65536, (N+1)^2 = 4,295,098,369 points per
+array -- past 2^31 and 2^32 elements, where the reference's int index math
+overflows (/root/reference/multigrid.cpp:77,83,138 and gs.cpp:228-292
+index with int n).
+
+No whole-field reference exists at this size (a field is 34 GB), so each
+check copies a few row slabs to the host and compares them with the CPU
+checker's row-slab forms of the same ops (oracle/mg_oracle.c *_slab, pinned to
+the whole-field ops by tests/test_oracle.py::test_slab_ops_equal_whole_field).
+Slabs sit at the first rows, around row 32768 (element index 2^31) and at the
+last rows (indices above 2^32).  Bar: BITWISE on every row the slab
+determines; the norm to the summation-order tolerance against an fp64 torch
+reduction done in row chunks.
+"""
+import gc
+
+import numpy as np
+import pytest
+import torch
+
+from hpcclassmultigridproject_amd import Multigrid, _lib, gs, init_problem
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+N = 65536
+W = N + 1
+M = W * W
+NU = -4e-4
+K_DT, H = 1.0 / N / 10, 1.0 / N
+NORM_RTOL = 1e-11
+# (first row, rows) of each slab
+SLABS = [(0, 48), (32744, 48), (N + 1 - 48, 48)]
+
+
+def _free():
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+
+def _rows(t, r0, nr, w=W):
+    torch.cuda.synchronize()
+    return t[r0 * w:(r0 + nr) * w].cpu().numpy()
+
+
+@pytest.fixture(scope="module")
+def fields():
+    assert M > 2 ** 32
+    free, total = torch.cuda.mem_get_info()
+    if free < 190e9:
+        pytest.skip(f"needs ~190 GB of free HBM, {free / 1e9:.0f} GB free")
+    g = torch.Generator(device="cuda").manual_seed(20220501)
+    f = {}
+    for name, lim in (("u", 1.0), ("rhs", 1.0), ("v1", 3.2), ("v2", 3.2)):
+        f[name] = torch.empty(M, dtype=torch.float64, device="cuda").uniform_(-lim, lim,
+                                                                              generator=g)
+    yield f
+    f.clear()
+    _free()
+
+
+def test_seam_ops_N65536(fields, oracle_mod):
+    """gs.h ops on the reference layout: compute_rhs, residual + compute_norm,
+    gauss_seidel, restriction, prolongation."""
+    O = oracle_mod
+    O.set_threads(8)
+    u, rhs, v1, v2 = fields["u"], fields["rhs"], fields["v1"], fields["v2"]
+    before = {r0: {k: _rows(fields[k], r0, nr) for k in fields} for r0, nr in SLABS}
+    out = torch.empty(M, dtype=torch.float64, device="cuda")
+    try:
+        # compute_rhs / residual: exact on rows [r0+1, r0+nr-2] (interior only)
+        gs.compute_rhs(out, u, N, v1, v2, K_DT, NU, H)
+        for r0, nr in SLABS:
+            b = before[r0]
+            want = O.compute_rhs_slab(b["u"], N, r0, b["v1"], b["v2"], K_DT, NU, H)
+            got = _rows(out, r0, nr)
+            a, e = max(1, r0 + 1) - r0, min(N, r0 + nr - 1) - r0
+            assert np.array_equal(got[a * W:e * W].reshape(-1, W)[:, 1:N],
+                                  want[a * W:e * W].reshape(-1, W)[:, 1:N]), r0
+        gs.residual(out, u, rhs, N, v1, v2, K_DT, NU, H)
+        for r0, nr in SLABS:
+            b = before[r0]
+            want = O.residual_slab(b["u"], b["rhs"], N, r0, b["v1"], b["v2"], K_DT, NU, H)
+            got = _rows(out, r0, nr)
+            a, e = max(1, r0 + 1) - r0, min(N, r0 + nr - 1) - r0
+            assert np.array_equal(got[a * W:e * W].reshape(-1, W)[:, 1:N],
+                                  want[a * W:e * W].reshape(-1, W)[:, 1:N]), r0
+        # compute_norm over the 4.3e9-point interior vs an fp64 torch sum in chunks
+        norm = gs.compute_norm(out, N)
+        view = out.view(W, W)
+        acc = 0.0
+        for i0 in range(1, N, 4096):
+            i1 = min(N, i0 + 4096)
+            acc += float(view[i0:i1, 1:N].square().sum())
+        assert abs(norm - acc ** 0.5) <= NORM_RTOL * norm
+        # gauss_seidel in place on u: exact on rows [r0+2, r0+nr-3]
+        w = u.clone()
+        gs.gauss_seidel(w, rhs, N, v1, v2, K_DT, NU, H)
+        for r0, nr in SLABS:
+            b = before[r0]
+            want = O.gauss_seidel_slab(b["u"].copy(), b["rhs"], N, r0, b["v1"], b["v2"],
+                                       K_DT, NU, H)
+            got = _rows(w, r0, nr)
+            a = (r0 + 2 if r0 > 0 else 0) - r0
+            e = (min(N + 1, r0 + nr - 2) if r0 + nr <= N else N + 1) - r0
+            assert np.array_equal(got[a * W:e * W], want[a * W:e * W]), r0
+        del w
+        _free()
+        # restriction: coarse (N/2+1)^2 <- even rows/columns of u
+        nc = N // 2
+        c = torch.empty((nc + 1) ** 2, dtype=torch.float64, device="cuda")
+        gs.restriction(c, u, N)
+        for r0, nr in SLABS:
+            I0 = (r0 + 1) // 2
+            I1 = min(nc + 1, (r0 + nr + 1) // 2)
+            got = _rows(c, I0, I1 - I0, nc + 1).reshape(-1, nc + 1)
+            want = before[r0]["u"].reshape(-1, W)[2 * I0 - r0:2 * I1 - r0:2, ::2]
+            assert np.array_equal(got, want), r0
+        # prolongation: fine (2 nc + 1)^2 = M points from the coarse field c
+        gs.prolongation(out, c, nc)
+        for I0, cn in ((0, 24), (16372, 24), (nc + 1 - 24, 24)):
+            crow = _rows(c, I0, cn, nc + 1)
+            want = O.prolongation_slab(crow, nc, I0)
+            got = _rows(out, 2 * I0, want.size // W)
+            assert np.array_equal(got, want), I0
+        del c
+    finally:
+        del out
+        _free()
+
+
+def test_fused_context_pass_N65536(oracle_mod):
+    """The product's tower-layout kernels at C5 size: a one-level context
+    (u, u', rhs, v1, v2: 5 x 34 GB), compute_rhs then ONE temporally blocked
+    pass of 3 RB-GS sweeps (the wave-private row march, 64-bit row offsets,
+    pitch 65552), checked on row slabs against compute_rhs + 3 gauss_seidel."""
+    free, _ = torch.cuda.mem_get_info()
+    if free < 190e9:
+        pytest.skip(f"needs ~190 GB of free HBM, {free / 1e9:.0f} GB free")
+    O = oracle_mod
+    O.set_threads(8)
+    u0, v1, v2 = init_problem(N, nthreads=16)
+    before = {r0: (u0[r0 * W:(r0 + nr) * W].copy(), v1[r0 * W:(r0 + nr) * W].copy(),
+                   v2[r0 * W:(r0 + nr) * W].copy()) for r0, nr in SLABS}
+    with Multigrid(N, 1, K_DT, NU, tower_mode=_lib.TOWER_CORRECT) as mg:
+        mg.upload(u0, v1, v2)
+        del v1, v2
+        mg.rhs()
+        mg.gs(0, 3)
+        u = mg.download(u0)
+    for r0, nr in SLABS:
+        bu, b1, b2 = before[r0]
+        rhs = O.compute_rhs_slab(bu, N, r0, b1, b2, K_DT, NU, H)
+        want = bu.copy()
+        for _ in range(3):
+            O.gauss_seidel_slab(want, rhs, N, r0, b1, b2, K_DT, NU, H)
+        # rhs exact on [r0+1, r0+nr-2]; each sweep loses 2 rows per side
+        a = (r0 + 1 + 6 if r0 > 0 else 0) - r0
+        e = (r0 + nr - 2 - 6 if r0 + nr <= N else N + 1) - r0
+        got = u[r0 * W:(r0 + nr) * W]
+        assert np.array_equal(got[a * W:e * W], want[a * W:e * W]), r0
+    del u, u0
+    _free()

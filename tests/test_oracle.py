@@ -184,3 +184,33 @@ def test_restatement_equals_reference_nu2(oracle_mod, N, maxlvl):
 def test_config2_summary_from_nu2_reference(golden_summary):
     s = golden_summary["steps"]["N4096_L3_nu2_2steps"]
     assert s["nsmooth"] == 2 and s["cycles"] == [2, 2]   # C2, 2 cycles/step
+
+
+@pytest.mark.parametrize("N,r0,nr", [(64, 0, 12), (64, 20, 9), (64, 55, 10), (64, 0, 65),
+                                     (33, 17, 17)])
+def test_slab_ops_equal_whole_field(oracle_mod, N, r0, nr):
+    """The row-slab forms (the N=65536 GPU checks' oracle) are the whole-field
+    ops on the rows their window determines, seeded random fields."""
+    O = oracle_mod
+    rng = np.random.default_rng(20220501)
+    w = N + 1
+    u, rhs = rng.uniform(-1, 1, w * w), rng.uniform(-1, 1, w * w)
+    v1, v2 = rng.uniform(-3, 3, w * w), rng.uniform(-3, 3, w * w)
+    k, h = 1.0 / N / 10, 1.0 / N
+    sl = slice(r0 * w, (r0 + nr) * w)
+    full = O.gauss_seidel(u.copy(), rhs, N, v1, v2, k, NU, h)
+    slab = O.gauss_seidel_slab(u[sl].copy(), rhs[sl], N, r0, v1[sl], v2[sl], k, NU, h)
+    a, b = (r0 + 2 if r0 > 0 else 0), min(N + 1, r0 + nr - 2 if r0 + nr <= N else N + 1)
+    assert np.array_equal(slab[(a - r0) * w:(b - r0) * w], full[a * w:b * w])
+    res_f = O.residual(u, rhs, N, v1, v2, k, NU, h)
+    res_s = O.residual_slab(u[sl].copy(), rhs[sl], N, r0, v1[sl], v2[sl], k, NU, h)
+    a1, b1 = max(1, r0 + 1), min(N, r0 + nr - 1)
+    assert np.array_equal(res_s[(a1 - r0) * w:(b1 - r0) * w], res_f[a1 * w:b1 * w])
+    crhs_f = O.compute_rhs(u, N, v1, v2, k, NU, h)
+    crhs_s = O.compute_rhs_slab(u[sl].copy(), N, r0, v1[sl], v2[sl], k, NU, h)
+    assert np.array_equal(crhs_s[(a1 - r0) * w:(b1 - r0) * w], crhs_f[a1 * w:b1 * w])
+    W = 2 * N + 1
+    pf = O.prolongation(u, N)
+    ps = O.prolongation_slab(u[sl].copy(), N, r0)
+    I1 = min(2 * (r0 + nr - 1), 2 * N)
+    assert np.array_equal(ps, pf[2 * r0 * W:(I1 + 1) * W])
