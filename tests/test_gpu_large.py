@@ -42,7 +42,7 @@ def _rows(t, r0, nr, w=W):
     return t[r0 * w:(r0 + nr) * w].cpu().numpy()
 
 
-@pytest.fixture(scope="module")
+@pytest.fixture
 def fields():
     assert M > 2 ** 32
     free, total = torch.cuda.mem_get_info()
