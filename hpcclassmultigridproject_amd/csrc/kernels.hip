@@ -98,6 +98,15 @@ __device__ __forceinline__ void st2s(double *p, double2 v) {
     st2(p, v);
 #endif
 }
+// Conditional stores of the march (exec-masked).  A hardware-dropped raw
+// buffer store (offset past the row) would avoid the exec branch, but measured
+// +20 % on the cross pass (3.25 vs 2.72 ms at N=16384), so these stay plain.
+__device__ __forceinline__ void st2_if(double *row, int col, bool on, double2 v) {
+    if (on) st2(row + col, v);
+}
+__device__ __forceinline__ void st1_if(double *row, int col, bool on, double v) {
+    if (on) row[col] = v;
+}
 __device__ __forceinline__ double sel(double2 p, int s) {
     const double x = p.x, y = p.y;
     return s ? y : x;
@@ -838,12 +847,14 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
 //
 // Workgroup = WPB pairs of waves on WPB adjacent strips.  In each pair, wave
 // A runs the k_wsmooth march of the post-smoothing (prolongation + add on
-// load, K sweeps, residual-norm partials) and wave B, D = S+2 rows behind,
+// load, K sweeps, residual-norm partials) and wave B, D = S+4 rows behind,
 // the march of the next pre-smoothing (K sweeps, residual restricted to the
 // coarse rhs).  A hands B each finished u row and each rhs / v row through a
-// small LDS ring (one lane to the same lane: no bank conflicts); one barrier
-// per step keeps the pair D rows apart.  Register footprint per wave = that
-// of one K-sweep march.  A also stores u_post (the solution after cycle k,
+// small LDS ring (one lane to the same lane: no bank conflicts).  The march
+// advances in PAIRS of steps: one barrier and one exit test per pair keep the
+// waves D rows apart (B reads only rows A wrote in an earlier pair; half the
+// barriers of a per-step hand-off: -2.5 % on the pass).  Register footprint
+// per wave = that of one K-sweep march.  A also stores u_post (the solution after cycle k,
 // which mg_outer returns if cycle k converged); B stores u_pre (cycle k+1
 // after its pre-smoothing).  Exactness: B's output strip needs A's output
 // on a cone EB = S+1 wider, A's on S more: H = ceil((S+EB)/2) halo pairs.
@@ -855,13 +866,18 @@ struct XCfg {
     static constexpr int H = (S + EB + 1) / 2;   // halo pairs per side
     static constexpr int NR = S + 4;             // register rings / unroll period
     static constexpr int W = 2 * (64 - 2 * H);
-    static constexpr int D = S + 2;              // B's lag in rows
-    static constexpr int NU = 4, NRD = 8;        // LDS hand-off rings (rows)
+    static constexpr int D = S + 4;              // B's lag in rows
+    // LDS hand-off rings, sizes dividing NR so every slot index is static.
+    // Per pair of steps A writes u rows s+2-S, s+3-S and rhs/v rows s+1, s+2;
+    // B reads u rows s-S-1, s-S and rhs/v rows s-S-1, s-S: spans of 5 and
+    // S+4 = NR rows, no slot written and read in the same pair.
+    static constexpr int NU = (NR % 5 == 0) ? 5 : NR, NRD = NR;
     // Rows an unguarded march may own: its warm-up reaches EA + EB + NR + D +
     // S rows above its first owned row and its drain D + EB + NR + 5 below its
     // last (B's garbage-in warm-up steps included), all of which must be rows
     // in [1, n-1] so that no update ever lands on a Dirichlet row.
-    static constexpr int TOP = EA + EB + NR + D + S + 2, BOT = D + EB + NR + 6;
+    // (+1: the march runs an even number of steps)
+    static constexpr int TOP = EA + EB + NR + D + S + 2, BOT = D + EB + NR + 7;
 };
 
 
@@ -982,10 +998,12 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
 
         // A's first step (aligned to NR so ring indices and parities are
         // static); B runs D steps behind; the last iteration is B's last step
+        // (rounded up to whole pairs: an extra step stores nothing)
         int s0 = a - EB - EA;
         s0 = s0 >= 0 ? (s0 / NR) * NR : -(((-s0) + NR - 1) / NR) * NR;
         s0 = __builtin_amdgcn_readfirstlane(s0);
-        const int iters = (b + EB - 3) + D - s0 + 1;
+        const int iters = ((b + EB - 3) + D - s0 + 1 + 1) & ~1;
+        const bool post = store_post != 0;
 
         double2 ur[NR];
         RowData rd[NR];
@@ -1009,8 +1027,8 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             load_rv(s0 + 2, rd[2]);
             for (;;) {
 #pragma unroll
-                for (int p = 0; p < NR; ++p) {
-                    const int s = s0 + it;
+                for (int p = 0; p < NR; ++p) {   // s == p (mod NR)
+                    const int s = s0 + it + (p & 1);
                     ur[(p + 3) % NR] = make_u(s + 3, up[(p + 1) & 1], (p + 3) & 1);
                     load_u(s + 5, up[(p + 1) & 1]);
 #pragma unroll
@@ -1018,7 +1036,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                     // hand-off: rhs/v row s+1 (first used above), final u row s+2-S
                     {
                         const RowData &dh = rd[(p + 1) % NR];
-                        double2(*slot)[64] = rdring[pr][(s + 1) & (NRD - 1)];
+                        double2(*slot)[64] = rdring[pr][(p + 1) % NRD];
                         slot[0][l] = dh.r;
                         slot[1][l] = dh.x;
                         slot[2][l] = dh.y;
@@ -1026,13 +1044,16 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                     {
                         const int ro = s + 2 - S;
                         const double2 uf = ur[(p + 2 - S + 2 * NR) % NR];
-                        uring[pr][ro & (NU - 1)][l] = uf;
-                        if (store_post && ro >= a && ro < b && keep)
-                            st2((upost + (long)ro * pitch) + c0, uf);
+                        uring[pr][(p + 2 - S + 2 * NR) % NU][l] = uf;
+                        st2_if(upost + (long)ro * pitch, c0, post && ro >= a && ro < b && keep,
+                               uf);
                     }
                     load_rv(s + 3, rd[(p + 3) % NR]);
-                    __syncthreads();
-                    if (++it == iters) goto done_a;
+                    if (p & 1) {   // end of a pair (compile-time)
+                        __syncthreads();
+                        it += 2;
+                        if (it >= iters) goto done_a;
+                    }
                 }
             }
         done_a:;
@@ -1040,13 +1061,13 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             for (;;) {
 #pragma unroll
                 for (int p = 0; p < NR; ++p) {
-                    const int s = s0 + it - D;   // B's ring phase q = p - D (mod NR)
+                    const int s = s0 + it + (p & 1) - D;   // B's ring phase q = p - D (mod NR)
                     constexpr int dq = ((D % NR) + NR) % NR;
                     const int q = (p - dq + NR) % NR;   // compile-time after unrolling
-                    // u row s+3 (A finished it last step) and rhs/v row s+3
-                    ur[(q + 3) % NR] = uring[pr][(s + 3) & (NU - 1)][l];
+                    // u row s+3 (A finished it in an earlier pair) and rhs/v row s+3
+                    ur[(q + 3) % NR] = uring[pr][(q + 3) % NU][l];
                     {
-                        double2(*slot)[64] = rdring[pr][(s + 3) & (NRD - 1)];
+                        double2(*slot)[64] = rdring[pr][(q + 3) % NRD];
                         rd[(q + 3) % NR].r = slot[0][l];
                         rd[(q + 3) % NR].x = slot[1][l];
                         rd[(q + 3) % NR].y = slot[2][l];
@@ -1059,58 +1080,57 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         const RowData &d = rd[iR];
                         const double uW = dpp_shr1(ur[iR].y);
                         const double uE = dpp_shl1(ur[iR].x);
-                        if (r >= a && r < b) {
-                            if (GN) {
-                                if (keep && r >= 1 && r <= n - 1) {
-                                    if (in0) {
-                                        const double res =
-                                            res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x, ur[iN].x,
-                                                        uW, ur[iS].x, ur[iR].y, c);
-                                        acc += res * res;
-                                    }
-                                    if (in1) {
-                                        const double res =
-                                            res_point_t(d.r.y, d.x.y, d.y.y, ur[iR].y, ur[iN].y,
-                                                        ur[iR].x, ur[iS].y, uE, c);
-                                        acc += res * res;
-                                    }
+                        const bool rin = r >= a && r < b;
+                        if (GN) {
+                            if (rin && keep && r >= 1 && r <= n - 1) {
+                                if (in0) {
+                                    const double res =
+                                        res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x, ur[iN].x,
+                                                    uW, ur[iS].x, ur[iR].y, c);
+                                    acc += res * res;
                                 }
-                            } else {   // acc + 0.0 == acc (acc >= +0): selects, no branch
-                                const double r0 = res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x,
-                                                              ur[iN].x, uW, ur[iS].x, ur[iR].y,
-                                                              c);
-                                const double r1 = res_point_t(d.r.y, d.x.y, d.y.y, ur[iR].y,
-                                                              ur[iN].y, ur[iR].x, ur[iS].y, uE,
-                                                              c);
-                                acc += keep ? r0 * r0 : 0.0;
-                                acc += keep ? r1 * r1 : 0.0;
+                                if (in1) {
+                                    const double res =
+                                        res_point_t(d.r.y, d.x.y, d.y.y, ur[iR].y, ur[iN].y,
+                                                    ur[iR].x, ur[iS].y, uE, c);
+                                    acc += res * res;
+                                }
                             }
+                        } else {   // acc + 0.0 == acc (acc >= +0): selects, no branch
+                            const double r0 = res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x,
+                                                          ur[iN].x, uW, ur[iS].x, ur[iR].y, c);
+                            const double r1 = res_point_t(d.r.y, d.x.y, d.y.y, ur[iR].y,
+                                                          ur[iN].y, ur[iR].x, ur[iS].y, uE, c);
+                            acc += (keep && rin) ? r0 * r0 : 0.0;
+                            acc += (keep && rin) ? r1 * r1 : 0.0;
                         }
                     }
 #pragma unroll
                     for (int h = 0; h < S; ++h) stage(ur, rd, q, h, s + 1 - h);
                     {
                         const int ro = s + 2 - S;
-                        if (ro >= a && ro < b && keep)
-                            st2((upre + (long)ro * pitch) + c0,
-                                ur[(q + 2 - S + 2 * NR) % NR]);
+                        st2_if(upre + (long)ro * pitch, c0, ro >= a && ro < b && keep,
+                               ur[(q + 2 - S + 2 * NR) % NR]);
                     }
-                    {   // residual -> coarse rhs at the even-even points (:73-75)
+                    if (((q + 1 - S) & 1) == 0) {   // compile-time row parity
+                        // residual -> coarse rhs at the even-even points (:73-75)
                         const int r = s + 1 - S;
                         const int iR = (q + 1 - S + 2 * NR) % NR;
                         const int iN = (q - S + 2 * NR) % NR;
                         const int iS = (q + 2 - S + 2 * NR) % NR;
                         const RowData &d = rd[iR];
                         const double uW = dpp_shr1(ur[iR].y);
-                        if (((q + 1 - S) & 1) == 0 && r >= a && r < b && keep &&
-                            (!GN || (r >= 1 && r <= n - 2 && in0 && c0 <= n - 2))) {
-                            const double res = res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x,
-                                                           ur[iN].x, uW, ur[iS].x, ur[iR].y, c);
-                            (rhsc + (long)(r >> 1) * pitchc)[c0 >> 1] = res;
-                        }
+                        const bool on = r >= a && r < b && keep &&
+                                        (!GN || (r >= 1 && r <= n - 2 && in0 && c0 <= n - 2));
+                        const double res = res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x, ur[iN].x,
+                                                       uW, ur[iS].x, ur[iR].y, c);
+                        st1_if(rhsc + (long)(r >> 1) * pitchc, c0 >> 1, on, res);
                     }
-                    __syncthreads();
-                    if (++it == iters) goto done_b;
+                    if (p & 1) {
+                        __syncthreads();
+                        it += 2;
+                        if (it >= iters) goto done_b;
+                    }
                 }
             }
         done_b:;
