@@ -39,9 +39,12 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
+
+import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -119,6 +122,12 @@ def parse():
                     help="multi-GPU: each rank builds only its rows (auto: N > 16384)")
     ap.add_argument("--no-profile", action="store_true",
                     help="do not record per-kernel HIP events in the timed region")
+    ap.add_argument("--sweep", nargs=2, type=int, metavar=("NMIN", "NMAX"),
+                    help="instead of the bench line: the 100-step time stepper for N = NMIN.."
+                         "NMAX (powers of two) on the GPU and the reference on the host, "
+                         "serial and all usable cores; writes cudatime.txt, serialtime.txt, "
+                         "omptime.txt ('N<TAB>seconds', what speedupplot.py reads)")
+    ap.add_argument("--sweep-out", default="", help="--sweep: output file prefix")
     return ap.parse_args()
 
 
@@ -198,8 +207,50 @@ def cpu_baseline(args):
                       f"rate); value = the fastest leg at N={N}"}
 
 
+def sweep(args):
+    """speedupplot.py's three inputs (/root/reference/speedupplot.py:10,25,40):
+    wall seconds of the 100-step time stepper per N, GPU (mgx_timestepper, as
+    mg_timer.cu times it: setup + steps + copy back) and the reference
+    timestepper on the host (oracle/_ref, the cpu_baseline leg's build), 1
+    thread and every usable core (multigrid.cpp:244-258 method)."""
+    import hpcclassmultigridproject_amd as pkg
+    from oracle import oracle as O
+    if not O.ref_available():
+        sys.exit("--sweep needs the compiled reference (oracle/_ref)")
+    cores = host_cpus()["usable"]
+    files = {k: open(args.sweep_out + k + "time.txt", "w") for k in ("cuda", "serial", "omp")}
+    out = {"sweep": [], "cores": cores}
+    N = args.sweep[0]
+    while N <= args.sweep[1]:
+        L = max(1, int(math.log2(N)) - 4)
+        dx = 1.0 / N
+        dt, nu = dx / 10, -4e-4
+        T = 100 * dt
+        u0, v1, v2 = pkg.init_problem(N)
+        uT = np.empty_like(u0)
+        t0 = time.perf_counter()
+        pkg.timestepper(uT, u0, v1, v2, nu, L, N, dt, T, dx, 1e-6)
+        tg = time.perf_counter() - t0
+        row = {"N": N, "cuda": tg}
+        for key, th in (("serial", 1), ("omp", cores)):
+            t0 = time.perf_counter()
+            ref = O.ref_timestepper(u0, v1, v2, nu, L, N, dt, T, dx, nthreads=th)
+            row[key] = time.perf_counter() - t0
+            row[key + "_bitwise"] = bool(np.array_equal(ref, uT))
+        for k, f in files.items():
+            f.write(f"{N}\t{row[k]:f}\n")
+            f.flush()
+        out["sweep"].append(row)
+        N *= 2
+    for f in files.values():
+        f.close()
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
+    if args.sweep:
+        return sweep(args)
     import torch
     import torch.distributed as dist
 

@@ -143,7 +143,10 @@ int main(int argc, char **argv) {
     timestepper(uTref.data(), u0.data(), v1.data(), v2.data(), nu, maxlvl, N, dt, T, tol, shape,
                 nsmooth, tower);
     double s1 = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    printf("\nGPU (MI355X, op-level control flow) time, N = %li: %f s\n", N, s1);
+    // the reference's three stdout lines (multigrid.cpp:246, :259, :266), with
+    // the labels saying what ran: its 1-thread reference leg is here the
+    // reference's op sequence on one GPU, its OMP leg the fused library path
+    printf("\nGPU (1 MI355X, reference op sequence) time, N = %i: %f s\n", (int)N, s1);
 
     mgx_options o;
     mgx_default_options(&o);
@@ -155,7 +158,7 @@ int main(int argc, char **argv) {
                            dx, tol, &o, nullptr),
         "mgx_timestepper");
     double s2 = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    printf("\nGPU (MI355X, mgx_timestepper) time, N = %li: %f s\n", N, s2);
+    printf("\nGPU with fused passes (%d MI355X) time, N = %i: %f s\n", 1, (int)N, s2);
     double error = 0;
     for (size_t p = 0; p < cnt; ++p) error += fabs(uTfast[p] - uTref[p]);
     printf("Error (compared to the referenced solution) = %10e\n", error);

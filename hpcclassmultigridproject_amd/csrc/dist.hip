@@ -31,12 +31,26 @@
 #include <vector>
 
 #include "ctx.h"
+#include "plan.h"
 
 namespace mgxi {
 
-constexpr int kGhost = 8;        // >= the widest fused-pass cone (E <= 7) + 1
-constexpr int kGhostFine = 16;   // level 0: the cross-cycle pass's cone is 14 rows
 long g_dist_min_rows = 256;
+
+// the partition / exchange plan (plan.h, host-only)
+using mgxplan::alloc_rows;
+using mgxplan::gather_rows;
+using mgxplan::ghost_plan;
+using mgxplan::kGhost;
+using mgxplan::plan_rows;
+using mgxplan::Xfer;
+static int plan_la(long n0, int L, int world) {
+    return mgxplan::plan_la(n0, L, world, g_dist_min_rows);
+}
+static int plan_check(long n0, int l, int world) {
+    const std::string e = mgxplan::plan_check(n0, l, world);
+    return e.empty() ? MGX_OK : fail(MGX_E_INTERNAL, e);
+}
 
 #define NCCLCHK(expr)                                                                    \
     do {                                                                                 \
@@ -79,31 +93,6 @@ struct Dist {
     double *hsum = nullptr;    // pinned
 };
 
-// Partition plan: rows of level l owned by `rank` (same rule on every rank).
-static void plan_rows(long n0, int l, int world, int rank, int *ra, int *rb) {
-    const long nl = n0 >> l;
-    const long q = nl / world;
-    *ra = (int)(rank * q);
-    *rb = rank == world - 1 ? (int)nl + 1 : (int)((rank + 1) * q);
-}
-
-static int plan_la(long n0, int L, int world) {
-    if (world <= 1) return L - 1 > 0 ? L - 1 : 0;
-    int la = 0;
-    while (la < L - 1 && ((n0 >> la) / world) >= g_dist_min_rows) ++la;
-    return la;
-}
-
-static int ghost_width(int l) { return l == 0 ? kGhostFine : kGhost; }
-
-// allocated rows [lo, hi] of `rank` on level l: owned + ghosts, clipped
-static void alloc_rows(long n0, int l, int world, int rank, int *ra, int *rb, int *lo, int *hi) {
-    plan_rows(n0, l, world, rank, ra, rb);
-    const int g = ghost_width(l);
-    *lo = std::max(0, *ra - g);
-    *hi = (int)std::min<long>(n0 >> l, (long)*rb - 1 + g);
-}
-
 void dist_free(mgx_ctx *c) {
     Dist *d = c->dist;
     if (!d) return;
@@ -123,17 +112,6 @@ void dist_free(mgx_ctx *c) {
     if (d->hsum) (void)hipHostFree(d->hsum);
     delete d;
     c->dist = nullptr;
-}
-
-static int plan_check(long n0, int l, int world);
-
-// The all-gather into the first replicated level la: rank r contributes rows
-// [r*q, (r+1)*q), q = n_la / world (what its restriction from its level la-1
-// block writes; row n_la, the boundary, is never read), in place, rank-major.
-static void gather_rows(long n0, int la, int world, int rank, long *row0, long *rows) {
-    const long q = (n0 >> la) / world;
-    *row0 = rank * q;
-    *rows = q;
 }
 
 static int build_dist(mgx_ctx *c, int world, const std::vector<int> &ranks) {
@@ -182,74 +160,6 @@ static double *field(const PLevel &L, Field f) {
         case kV1: return L.F(L.v1);
         default: return L.F(L.v2);
     }
-}
-
-// ---- exchange plan.  ONE host-side description of every ghost-row transfer,
-// consumed by both transports: RCCL posts each entry as an ncclSend of its
-// send rows + an ncclRecv into its recv rows; the local (virtual-rank)
-// transport pairs each entry with the peer's entry for this rank and copies
-// sender rows -> receiver rows after checking that the two agree.  So the
-// single-GPU parity tests execute exactly the offsets / counts the RCCL ranks
-// post, and tests/test_capi.py checks the plan's symmetry on the CPU
-// (mgx_exchange_plan).  Rows are global row indices of the level.
-struct Xfer {
-    int peer;
-    int send_row, send_rows;   // send rows [send_row, +send_rows) to peer
-    int recv_row, recv_rows;   // receive rows [recv_row, +recv_rows) from it
-};
-
-// Ghost rows of level l of `rank`: [lo, ra) come from rank-1 (its last owned
-// rows), [rb, hi] from rank+1 (its first owned rows); it sends each
-// neighbour the rows that neighbour's ghosts mirror.
-static void ghost_plan(long n0, int l, int world, int rank, std::vector<Xfer> &out) {
-    out.clear();
-    if (world <= 1) return;
-    int ra, rb, lo, hi;
-    alloc_rows(n0, l, world, rank, &ra, &rb, &lo, &hi);
-    for (int peer : {rank - 1, rank + 1}) {
-        if (peer < 0 || peer >= world) continue;
-        int pa, pb, plo, phi;
-        alloc_rows(n0, l, world, peer, &pa, &pb, &plo, &phi);
-        Xfer x;
-        x.peer = peer;
-        if (peer < rank) {   // its upper ghosts [pb, phi] = my first owned rows
-            x.send_row = pb;
-            x.send_rows = phi - pb + 1;
-            x.recv_row = lo;
-            x.recv_rows = ra - lo;
-        } else {             // its lower ghosts [plo, pa) = my last owned rows
-            x.send_row = plo;
-            x.send_rows = pa - plo;
-            x.recv_row = rb;
-            x.recv_rows = hi - rb + 1;
-        }
-        out.push_back(x);
-    }
-}
-
-// The plans of all ranks agree pairwise (what i sends j is what j receives
-// from i: same global rows, same count), sends read only owned rows, receives
-// land only in allocated ghost rows.
-static int plan_check(long n0, int l, int world) {
-    std::vector<std::vector<Xfer>> P(world);
-    for (int r = 0; r < world; ++r) ghost_plan(n0, l, world, r, P[r]);
-    for (int r = 0; r < world; ++r) {
-        int ra, rb, lo, hi;
-        alloc_rows(n0, l, world, r, &ra, &rb, &lo, &hi);
-        for (const Xfer &x : P[r]) {
-            if (x.send_rows <= 0 || x.send_row < ra || x.send_row + x.send_rows > rb)
-                return fail(MGX_E_INTERNAL, "exchange plan: send outside the owned rows");
-            if (x.recv_rows <= 0 || x.recv_row < lo || x.recv_row + x.recv_rows > hi + 1 ||
-                (x.recv_row < rb && x.recv_row + x.recv_rows > ra))
-                return fail(MGX_E_INTERNAL, "exchange plan: receive outside the ghost rows");
-            const Xfer *y = nullptr;
-            for (const Xfer &z : P[x.peer])
-                if (z.peer == r) y = &z;
-            if (!y || y->recv_row != x.send_row || y->recv_rows != x.send_rows)
-                return fail(MGX_E_INTERNAL, "exchange plan: peers disagree");
-        }
-    }
-    return MGX_OK;
 }
 
 // Refresh the ghost rows of the listed (level, field)s from the neighbouring

@@ -8,6 +8,7 @@ library's fast path.  ./mg_sweep writes cudatime.txt / gpups.txt in the
 "N<TAB>value" format speedupplot.py reads.
 """
 import os
+import re
 import subprocess
 
 import pytest
@@ -32,8 +33,14 @@ def test_multigrid_driver_writes_reference_uT(tmp_path):
     for name in ("uT.txt", "uTomp.txt"):
         with open(tmp_path / name) as f:
             assert f.read() == want, name
-    assert "time, N = 32:" in out
-    assert "Error (compared to the referenced solution) = 0.000000e+00" in out
+    # the reference's line shapes (multigrid.cpp:246, :259, :266):
+    # "\n<label> time, N = %i: %f s\n" twice, then the %10e error line
+    lines = out.split("\n")
+    timed = [l for l in lines if re.fullmatch(r".+ time, N = 32: \d+\.\d{6} s", l)]
+    assert len(timed) == 2, out
+    assert timed[0].startswith("GPU (1 MI355X") and timed[1].startswith("GPU with ")
+    assert lines[lines.index(timed[0]) - 1] == "" and lines[lines.index(timed[1]) - 1] == ""
+    assert "Error (compared to the referenced solution) = 0.000000e+00" in lines
 
 
 def test_mg_sweep_formats(tmp_path):
@@ -46,3 +53,21 @@ def test_mg_sweep_formats(tmp_path):
         rows = [l.split("\t") for l in open(tmp_path / name).read().splitlines()]
         assert [int(r[0]) for r in rows] == [32, 64, 128, 256]
         assert all(conv(r[1]) > 0 for r in rows)
+
+
+def test_bench_sweep_writes_speedupplot_inputs(tmp_path):
+    """bench.py --sweep: cudatime.txt / serialtime.txt / omptime.txt in the
+    'N<TAB>seconds' format speedupplot.py reads (/root/reference/speedupplot.py
+    :10,25,40); the GPU and the reference's serial and OpenMP runs agree bitwise."""
+    import json
+    import sys
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--sweep", "32", "64",
+                          "--sweep-out", str(tmp_path) + "/"], capture_output=True, text=True,
+                         timeout=300, check=True).stdout
+    rec = json.loads(out.strip().splitlines()[-1])
+    assert [r["N"] for r in rec["sweep"]] == [32, 64]
+    assert all(r["serial_bitwise"] and r["omp_bitwise"] for r in rec["sweep"])
+    for name in ("cudatime.txt", "serialtime.txt", "omptime.txt"):
+        rows = [l.split("\t") for l in open(tmp_path / name).read().splitlines()]
+        assert [int(r[0]) for r in rows] == [32, 64]
+        assert all(float(r[1]) > 0 for r in rows)
