@@ -139,6 +139,9 @@ int dist_la(mgx_ctx *c);
 // levels whose row blocks would be shorter than this are replicated (tuning
 // key "dist_min_rows", default 256)
 extern long g_dist_min_rows;
+// tuning key "dist_overlap" (dist.hip): finest-level ghost exchange on a second
+// stream beside the interior of the cross-cycle pass
+extern long g_dist_overlap;
 // tuning key "cross_cycle" (mgx.hip); levels with n >= kCrossMinN can use it
 bool cross_cycle_on();
 constexpr long kCrossMinN = 4096;

@@ -36,12 +36,17 @@
 namespace mgxi {
 
 long g_dist_min_rows = 256;
+// tuning key "dist_overlap": 1 = the finest level's ghost exchange runs on a
+// second stream while the cross-cycle pass updates the rows whose cone stays
+// inside the block; the two ghost-dependent bands follow the exchange
+long g_dist_overlap = 0;
 
 // the partition / exchange plan (plan.h, host-only)
 using mgxplan::alloc_rows;
 using mgxplan::gather_rows;
 using mgxplan::ghost_plan;
 using mgxplan::kGhost;
+using mgxplan::kGhostFine;
 using mgxplan::plan_rows;
 using mgxplan::Xfer;
 static int plan_la(long n0, int L, int world) {
@@ -91,6 +96,9 @@ struct Dist {
     std::vector<Part> parts;   // local: `world` parts; RCCL: this rank's part
     ncclComm_t comm = nullptr;
     double *hsum = nullptr;    // pinned
+    // dist_overlap: ghost exchanges on a second stream beside the interior pass
+    hipStream_t xs = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 void dist_free(mgx_ctx *c) {
@@ -109,6 +117,9 @@ void dist_free(mgx_ctx *c) {
         (void)hipFree(p.dsum);
     }
     if (d->comm) (void)ncclCommDestroy(d->comm);
+    if (d->xs) (void)hipStreamDestroy(d->xs);
+    if (d->ev_fork) (void)hipEventDestroy(d->ev_fork);
+    if (d->ev_join) (void)hipEventDestroy(d->ev_join);
     if (d->hsum) (void)hipHostFree(d->hsum);
     delete d;
     c->dist = nullptr;
@@ -120,6 +131,9 @@ static int build_dist(mgx_ctx *c, int world, const std::vector<int> &ranks) {
     d->la = plan_la(c->N, c->L, world);
     for (int l = 0; l < d->la; ++l) CHK(plan_check(c->N, l, world));
     HIPCHK(hipHostMalloc(&d->hsum, sizeof(double) * 8));
+    HIPCHK(hipStreamCreateWithFlags(&d->xs, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming));
     for (int r : ranks) {
         Part p;
         p.rank = r;
@@ -169,7 +183,7 @@ struct XF {
     Field f;
 };
 
-static int exchange_rows(mgx_ctx *c, std::initializer_list<XF> xs) {
+static int exchange_rows(mgx_ctx *c, std::initializer_list<XF> xs, hipStream_t st) {
     Dist *d = c->dist;
     std::vector<Xfer> plan;
     if (d->local) {
@@ -185,7 +199,7 @@ static int exchange_rows(mgx_ctx *c, std::initializer_list<XF> xs) {
                     HIPCHK(hipMemcpyAsync(field(R, x.f) + (long)t.send_row * P,
                                           field(L, x.f) + (long)t.send_row * P,
                                           sizeof(double) * (size_t)t.send_rows * P,
-                                          hipMemcpyDeviceToDevice, c->stream));
+                                          hipMemcpyDeviceToDevice, st));
                 }
             }
         return MGX_OK;
@@ -200,10 +214,10 @@ static int exchange_rows(mgx_ctx *c, std::initializer_list<XF> xs) {
         for (const Xfer &t : plan) {
             if (r != ncclSuccess) break;
             r = ncclSend(a + (long)t.send_row * P, (size_t)t.send_rows * P, ncclDouble, t.peer,
-                         d->comm, c->stream);
+                         d->comm, st);
             if (r == ncclSuccess)
                 r = ncclRecv(a + (long)t.recv_row * P, (size_t)t.recv_rows * P, ncclDouble,
-                             t.peer, d->comm, c->stream);
+                             t.peer, d->comm, st);
         }
     }
     const ncclResult_t re = ncclGroupEnd();   // always close the group
@@ -225,7 +239,8 @@ static int exchange(mgx_ctx *c, std::initializer_list<XF> xs) {
             ghost_plan(c->N, x.l, c->dist->world, p.rank, plan);
             for (const Xfer &t : plan) bytes += 16.0 * t.send_rows * p.lv[x.l].pitch;
         }
-    CHK(launch(c, MGX_K_HALO, xs.begin()->l, bytes, [&] { rc = exchange_rows(c, xs); }));
+    CHK(launch(c, MGX_K_HALO, xs.begin()->l, bytes,
+               [&] { rc = exchange_rows(c, xs, c->stream); }));
     return rc;
 }
 
@@ -410,17 +425,32 @@ static void dist_drop_spec(mgx_ctx *c) {
 // (16 rows: the pass's cone is 14) and, if level 1 is partitioned, its u
 // ghosts for the prolongation; afterwards the restricted rhs of the next cycle
 // is made ready on level 1 and the per-rank norm sums are reduced by the caller.
+//
+// dist_overlap = 1: the exchange goes on the second stream (forked after the
+// work that produced the sent rows) while the compute stream runs the pass
+// over rows [ra+16, rb-16) -- whose cone [ra+2, rb-2) and coarse parents are
+// all owned, so it needs no ghost row -- then, after the exchange, the two
+// 16-row bands next to the ghosts (norm partial sums accumulated).  Outputs,
+// u_pre / u_post / coarse rhs, are the same rows either way: bitwise.
 static int dist_cross(mgx_ctx *c, bool store_post) {
     Dist *d = c->dist;
-    if (1 < d->la)
-        CHK(exchange(c, {XF{0, kU}, XF{1, kU}}));
-    else
-        CHK(exchange(c, 0, kU));
-    for (auto &p : d->parts) {
+    const int G = kGhostFine;
+    const int k = c->opt.nsmooth;
+    bool ov = g_dist_overlap != 0 && d->world > 1;
+    for (auto &p : d->parts) ov = ov && p.lv[0].rb - p.lv[0].ra >= 4 * G;
+    auto xs = {XF{0, kU}, XF{1, kU}};
+    auto x0 = {XF{0, kU}};
+    if (ov) {
+        HIPCHK(hipEventRecord(d->ev_fork, c->stream));
+        HIPCHK(hipStreamWaitEvent(d->xs, d->ev_fork, 0));
+        CHK(exchange_rows(c, 1 < d->la ? xs : x0, d->xs));
+        HIPCHK(hipEventRecord(d->ev_join, d->xs));
+    } else {
+        CHK(exchange(c, 1 < d->la ? xs : x0));
+    }
+    // one launch of the pass over owned rows [ra, rb) of part p
+    auto pass = [&](Part &p, int P, int Q, int ra, int rb, bool accumulate) -> int {
         PLevel &L = p.lv[0];
-        int P = -1, Q = -1;
-        for (int i = 0; i < 3; ++i)
-            if (i != L.cur) (P < 0 ? P : Q) = i;
         mgx::XArgs A;
         A.uin = L.U();
         A.upost = L.F(L.u[P]);
@@ -434,34 +464,67 @@ static int dist_cross(mgx_ctx *c, bool store_post) {
             A.uc = Cl.U();
             A.rhsc = Cl.F(Cl.rhs);
             A.pitchc = Cl.pitch;
-            Mc = Cl.Mown();
         } else {
             Level &Cl = p.sub->lv[0];
             A.uc = Cl.U();
             A.rhsc = Cl.rhs;
             A.pitchc = Cl.pitch;
-            Mc = L.Mown() / 4;
         }
+        const double Mown = double(rb - ra) * double(L.n + 1);
+        Mc = Mown / 4;
         A.partials = c->partials;
         A.norm_out = p.dsum;
         A.norm_sqrt = false;
+        A.norm_accumulate = accumulate;
         A.n = L.n;
         A.pitch = L.pitch;
         A.c = L.coef;
         A.store_post = store_post;
-        A.ra = L.ra;
-        A.rb = L.rb;
+        A.ra = ra;
+        A.rb = rb;
         A.lo = L.lo;
         A.hi = L.hi;
-        const int k = c->opt.nsmooth;
-        const double bytes = (32.0 + 40.0 * k + 48.0 + 40.0 * k + 40.0) * L.Mown() + 32.0 * Mc;
-        const double cbytes = 8.0 * ((store_post ? 6.0 : 5.0) * L.Mown() + 2.0 * Mc);
+        if (rb - ra < 4 * G) A.min_rows = 8;   // a band: many short segments
+        const double bytes = (32.0 + 40.0 * k + 48.0 + 40.0 * k + 40.0) * Mown + 32.0 * Mc;
+        const double cbytes = 8.0 * ((store_post ? 6.0 : 5.0) * Mown + 2.0 * Mc);
         int blocks = 0;
         CHK(launch(c, MGX_K_XSMOOTH, 0, bytes, cbytes,
                    [&] { blocks = mgx::launch_xsmooth(A, k, c->stream); }));
         if (blocks < 0) return fail(MGX_E_ARG, "launch_xsmooth: unsupported sweeps / block");
-        L.cur = P;
-        L.spec = Q;
+        return MGX_OK;
+    };
+    std::vector<std::pair<int, int>> bufs;
+    for (auto &p : d->parts) {
+        PLevel &L = p.lv[0];
+        int P = -1, Q = -1;
+        for (int i = 0; i < 3; ++i)
+            if (i != L.cur) (P < 0 ? P : Q) = i;
+        bufs.push_back({P, Q});
+    }
+    if (!ov) {
+        for (size_t i = 0; i < d->parts.size(); ++i) {
+            PLevel &L = d->parts[i].lv[0];
+            CHK(pass(d->parts[i], bufs[i].first, bufs[i].second, L.ra, L.rb, false));
+        }
+    } else {
+        // bands start at even rows (the pass's row parity / restriction)
+        for (size_t i = 0; i < d->parts.size(); ++i) {
+            PLevel &L = d->parts[i].lv[0];
+            const int top = (L.rb - G) & ~1;
+            CHK(pass(d->parts[i], bufs[i].first, bufs[i].second, L.ra + G, top, false));
+        }
+        HIPCHK(hipStreamWaitEvent(c->stream, d->ev_join, 0));
+        for (size_t i = 0; i < d->parts.size(); ++i) {
+            PLevel &L = d->parts[i].lv[0];
+            const int top = (L.rb - G) & ~1;
+            CHK(pass(d->parts[i], bufs[i].first, bufs[i].second, L.ra, L.ra + G, true));
+            CHK(pass(d->parts[i], bufs[i].first, bufs[i].second, top, L.rb, true));
+        }
+    }
+    for (size_t i = 0; i < d->parts.size(); ++i) {
+        PLevel &L = d->parts[i].lv[0];
+        L.cur = bufs[i].first;
+        L.spec = bufs[i].second;
         L.zero = false;
     }
     return coarse_rhs_ready(c, 0);

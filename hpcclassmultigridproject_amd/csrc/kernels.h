@@ -75,6 +75,7 @@ struct SmoothArgs {
     double *partials;   // NORM
     double *norm_out;   // NORM: sqrt of the sum (norm_sqrt) or the plain sum
     bool norm_sqrt = true;
+    bool norm_accumulate = false;   // NORM: add the plain sum to *norm_out
     // Row-block partitions (multi-GPU): output rows [ra, rb) and rows [lo, hi]
     // that hold valid data (owned + ghost rows), all global row indices; the
     // field pointers are offset so that ptr + r*pitch is global row r.
@@ -101,7 +102,9 @@ struct XArgs {
     Coef c{};
     bool store_post = true;   // false: u_post only feeds the norm (not the last cycle)
     bool norm_sqrt = true;    // false: *norm_out = sum of squares (multi-GPU partial)
+    bool norm_accumulate = false;   // *norm_out += sum of squares (split pass)
     int ra = 0, rb = -1, lo = 0, hi = -1;   // row block (rb < 0: whole level), as SmoothArgs
+    int min_rows = 64;   // fewest rows per workgroup (short bands: smaller, more parallel)
 };
 int launch_xsmooth(const XArgs &a, int sweeps, hipStream_t s);
 // Cross pass: 1 = interior strips run the unguarded march (default), 0 = all guarded.

@@ -142,7 +142,9 @@ __global__ __launch_bounds__(kFinalThreads) void k_norm_final(const double *part
     double acc = 0.0;
     for (int i = threadIdx.x; i < count; i += kFinalThreads) acc += partials[i];
     double tot = block_sum(acc, lds);
-    if (threadIdx.x == 0) out[0] = take_sqrt ? sqrt(tot) : tot;
+    // take_sqrt: 1 = sqrt of the sum, 0 = the sum, 2 = add the sum to out[0]
+    // (a pass split into several launches on one stream, multi-GPU partials)
+    if (threadIdx.x == 0) out[0] = take_sqrt == 1 ? sqrt(tot) : take_sqrt == 2 ? out[0] + tot : tot;
 }
 
 // ============================================================ reference layout
@@ -1854,10 +1856,10 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
     const bool split = g_xfast != 0 && A.c.dgs > 0;
     march_regions<WPB>(n, X::W, X::H, ra, rb, X::TOP, X::BOT, split, inner, unused);
     march_regions<1>(n, X::W, X::H, ra, rb, X::TOP, X::BOT, split, unused, edge);
-    const int pm = xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, 64,
+    const int pm = xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, A.min_rows,
                                                  kNormBlocks / WPB / 2, s);
-    const int pe = xsmooth_launch<1, K, true>(A, edge, A.partials + pm, lo, hi, 32,
-                                              kNormBlocks / 2, s);
+    const int pe = xsmooth_launch<1, K, true>(A, edge, A.partials + pm, lo, hi,
+                                              std::min(32, A.min_rows), kNormBlocks / 2, s);
     return pm + pe;
 }
 
@@ -1874,7 +1876,7 @@ int launch_xsmooth(const XArgs &A, int sweeps, hipStream_t s) {
     }
     if (blocks > 0)
         MGX_LAUNCH(k_norm_final, dim3(1), dim3(kFinalThreads), s, (const double *)A.partials,
-                   blocks, A.norm_out, A.norm_sqrt ? 1 : 0);
+                   blocks, A.norm_out, A.norm_accumulate ? 2 : A.norm_sqrt ? 1 : 0);
     return blocks;
 }
 
@@ -2000,7 +2002,7 @@ int launch_smooth(const SmoothArgs &A0, int sweeps, int mode, hipStream_t s) {
     }
     if (blocks > 0 && (mode & 8))
         MGX_LAUNCH(k_norm_final, dim3(1), dim3(kFinalThreads), s, (const double *)A.partials,
-                   blocks, A.norm_out, A.norm_sqrt ? 1 : 0);
+                   blocks, A.norm_out, A.norm_accumulate ? 2 : A.norm_sqrt ? 1 : 0);
     return blocks;
 }
 

@@ -933,6 +933,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgxi::g_cross_cycle = value;
         return MGX_OK;
     }
+    if (!strcmp(key, "dist_overlap")) {
+        if (value != 0 && value != 1) return fail(MGX_E_ARG, "dist_overlap must be 0 or 1");
+        mgxi::g_dist_overlap = value;
+        return MGX_OK;
+    }
     if (!strcmp(key, "dist_min_rows")) {
         if (value < 16 || (value & 1)) return fail(MGX_E_ARG, "dist_min_rows must be even, >= 16");
         mgxi::g_dist_min_rows = value;
@@ -979,6 +984,10 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     if (!strcmp(key, "cross_cycle")) {
         mgxi::cross_cycle_on();
         *value = mgxi::g_cross_cycle;
+        return MGX_OK;
+    }
+    if (!strcmp(key, "dist_overlap")) {
+        *value = mgxi::g_dist_overlap;
         return MGX_OK;
     }
     if (!strcmp(key, "dist_min_rows")) {

@@ -168,6 +168,10 @@ int mgx_synchronize(mgx_ctx *ctx);
  * the next cycle's restricted rhs, not the last correction.  0 = off.
  * "dist_min_rows": partitioned solvers replicate every level whose row blocks
  * would be shorter than this (default 256, even, >= 16); read at creation.
+ * "dist_overlap": 1 = on partitioned contexts the finest level's ghost
+ * exchange runs on a second stream while the cross-cycle pass updates the
+ * rows whose cone stays inside the block; the two 16-row bands next to the
+ * ghosts follow the exchange (default 0; bitwise the same results).
  * "xfast": 1 (default) runs the cross-cycle pass as an unguarded kernel over
  * the interior strips and rows plus a guarded kernel over the boundary strips
  * and bands; 0 = one guarded launch (bitwise the same results).

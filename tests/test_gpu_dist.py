@@ -297,3 +297,47 @@ def test_C4_two_timesteps_partitioned_N16384(golden_summary, G):
     assert cyc == [3, 3]
     assert xs == 6 * G   # the cross-cycle pass ran on every block, every cycle
     assert hashlib.sha256(u.tobytes()).hexdigest() == s["sha256"]
+
+
+@pytest.fixture
+def overlap():
+    old = _lib.get_tuning("dist_overlap")
+    yield lambda v: _lib.set_tuning("dist_overlap", v)
+    _lib.set_tuning("dist_overlap", old)
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+def test_overlapped_exchange_bitwise(G, overlap):
+    """dist_overlap = 1 (finest ghost exchange on a second stream beside the
+    interior of the cross pass, then the two ghost bands) gives the same u
+    bitwise as the serialised schedule and as one GPU, norms to the
+    summation-order tolerance (the split pass adds three partial sums)."""
+    N, L = 4096, 7
+    dt = 1.0 / N / 10
+    us, ns, rs, _ = _run(N, L, dt, NU, 4)
+    out = {}
+    for ov in (0, 1):
+        overlap(ov)
+        out[ov] = _run(N, L, dt, NU, 4, parts=G)
+    for ov in (0, 1):
+        up, npart, rp, info = out[ov]
+        assert info[0] == G
+        assert np.array_equal(up, us), ov
+        np.testing.assert_allclose(npart, ns, rtol=NORM_RTOL)
+
+
+@pytest.mark.slow
+def test_C4_two_timesteps_overlapped_N16384(golden_summary, overlap):
+    """Config C4 with the overlapped exchange: 8 row blocks, two timesteps,
+    cycles [3, 3] and the reference's sha256."""
+    s = golden_summary["steps"]["N16384_L9_2steps"]
+    N, L = 16384, 9
+    overlap(1)
+    u0, v1, v2 = init_problem(N, nthreads=16)
+    with Multigrid(N, L, 1.0 / N / 10, NU, local_parts=8) as mg:
+        mg.upload(u0, v1, v2)
+        del v1, v2
+        cyc = [mg.step(1e-6) for _ in range(2)]
+        u = mg.download(u0)
+    assert cyc == [3, 3]
+    assert hashlib.sha256(u.tobytes()).hexdigest() == s["sha256"]

@@ -15,20 +15,26 @@ ap.add_argument('--parts', default='1,2,4,8')
 ap.add_argument('--cycles', type=int, default=5)
 ap.add_argument('--rounds', type=int, default=2)
 ap.add_argument('--min-rows', default='256')
+ap.add_argument('--overlap', default='0', help='dist_overlap values to compare, e.g. 0,1')
 a = ap.parse_args()
 N, L = a.N, a.L
 dt = 1.0 / N / 10
 u0, v1, v2 = pkg.init_problem(N, nthreads=16)
 for rnd in range(a.rounds):
   for mr in (int(x) for x in a.min_rows.split(',')):
-    _lib.set_tuning("dist_min_rows", mr)
+   _lib.set_tuning("dist_min_rows", mr)
+   for ov in (int(x) for x in a.overlap.split(',')):
+    _lib.set_tuning("dist_overlap", ov)
     for G in [int(x) for x in a.parts.split(',')]:
+        if G == 1 and ov:
+            continue
         mg = pkg.Multigrid(N, L, dt, -4e-4, device=0, local_parts=G if G > 1 else 0)
         mg.upload(u0, v1, v2); mg.rhs(); mg.run_cycles(1); mg.synchronize()
         mg.profile_reset(); mg.profile(True)
         t = time.perf_counter(); r = mg.run_cycles(a.cycles); mg.synchronize()
         ms = (time.perf_counter() - t) / a.cycles * 1e3
-        d = {"min_rows": mr, "G": G, "ms": round(ms, 3), "la": mg.dist_info()[2], "res": r}
+        d = {"min_rows": mr, "overlap": ov, "G": G, "ms": round(ms, 3),
+             "ms_per_rank": round(ms / G, 3), "la": mg.dist_info()[2], "res": r}
         for kind, name in _lib.KERNEL_NAMES.items():
             n, kms, _ = mg.profile_get(kind, -1)
             if n: d[name] = round(kms / a.cycles, 4)
