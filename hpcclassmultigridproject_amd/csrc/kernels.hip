@@ -462,6 +462,11 @@ __global__ __launch_bounds__(BLOCK) void k_gs_sweep(const double *__restrict__ u
 struct RowData {
     double2 r, x, y;
 };
+// the four coefficients of a row's two points (column c0 in .x, c0+1 in .y):
+// (rhs - cn*uN - cw*uW - cs*uS - ce*uE) / d, gs.cpp:126-130
+struct CoefRow {
+    double2 cn, cw, cs, ce;
+};
 
 // The sign of a/d is sign(a) xor sign(d), also for a = +-0 (where the fma
 // chain alone would return +0 for a = -0): one v_xor + v_bfi on the high word
@@ -1014,6 +1019,53 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             ur[q] = make_double2(0.0, 0.0);
             rd[q].r = rd[q].x = rd[q].y = make_double2(0.0, 0.0);
         }
+        // B turns each rhs/v row's t1, t2 into the four coefficients of its
+        // two points once (gs.cpp:126-129, the expressions of gs_point_t),
+        // just before the row's first stage, instead of in each of the
+        // point's three stages and its restriction residual: -12 % VALU per
+        // pass, -3 % time (the same in A as well: -23 % VALU, no further
+        // time, 254 instead of 224 VGPRs -- the pass is not issue bound)
+        CoefRow cf[NR];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+            const double2 z = make_double2(0.0, 0.0);
+            cf[i] = CoefRow{z, z, z, z};
+        }
+        auto to_coef = [&](const RowData &d, CoefRow &k) {
+            k.cn = make_double2(c.rr * (c.nu - d.x.x), c.rr * (c.nu - d.x.y));
+            k.cw = make_double2(c.rr * (c.nu - d.y.x), c.rr * (c.nu - d.y.y));
+            k.cs = make_double2(c.rr * (d.x.x + c.nu), c.rr * (d.x.y + c.nu));
+            k.ce = make_double2(c.rr * (d.y.x + c.nu), c.rr * (d.y.y + c.nu));
+        };
+        // stage h at ring phase q on row r (as `stage`), from the coefficients
+        auto stage_c = [&](const int q, const int h, const int r) {
+            const int iR = (q + 1 - h + 2 * NR) % NR;
+            const int iN = (q - h + 2 * NR) % NR;
+            const int iS = (q + 2 - h + 2 * NR) % NR;
+            const int cs = ((q + 1 - h) & 1) ^ (h & 1);
+            const CoefRow &k = cf[iR];
+            const double2 f = rd[iR].r;
+            const bool inr = !GS || (r >= 1 && r <= n - 1);
+            if (cs == 0) {
+                const double uW = dpp_shr1(ur[iR].y);
+                if (!GS || (inr && in0))
+                    ur[iR].x = div_diag<!GS>(f.x - k.cn.x * ur[iN].x - k.cw.x * uW -
+                                                 k.cs.x * ur[iS].x - k.ce.x * ur[iR].y,
+                                             c);
+            } else {
+                const double uE = dpp_shl1(ur[iR].x);
+                if (!GS || (inr && in1))
+                    ur[iR].y = div_diag<!GS>(f.y - k.cn.y * ur[iN].y - k.cw.y * ur[iR].x -
+                                                 k.cs.y * ur[iS].y - k.ce.y * uE,
+                                             c);
+            }
+        };
+        // residual (gs.cpp:75 term order) at column c0 of the row in slot iR
+        auto res_x = [&](const int iR, const int iN, const int iS, const double uW) {
+            const CoefRow &k = cf[iR];
+            return rd[iR].r.x - (c.dgs * ur[iR].x + k.cn.x * ur[iN].x + k.cw.x * uW +
+                                 k.cs.x * ur[iS].x + k.ce.x * ur[iR].y);
+        };
         // one loop per role (a role branch inside the step would make the
         // waitcnt pass see A's pending loads on B's path and drain them)
         int it = 0;
@@ -1050,6 +1102,29 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         st2_if(upost + (long)ro * pitch, c0, post && ro >= a && ro < b && keep,
                                uf);
                     }
+                    // residual norm of u_post (multigrid.cpp:112-113), column c0 of
+                    // row s+1-S (its neighbours are final now; B takes column c0+1:
+                    // half each balances the pair's VALU work)
+                    {
+                        const int r = s + 1 - S;
+                        const int iR = (p + 1 - S + 2 * NR) % NR;
+                        const int iN = (p - S + 2 * NR) % NR;
+                        const int iS = (p + 2 - S + 2 * NR) % NR;
+                        const RowData &d = rd[iR];
+                        const double uW = dpp_shr1(ur[iR].y);
+                        const bool rin = r >= a && r < b;
+                        if (GN) {
+                            if (rin && keep && r >= 1 && r <= n - 1 && in0) {
+                                const double res = res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x,
+                                                               ur[iN].x, uW, ur[iS].x, ur[iR].y, c);
+                                acc += res * res;
+                            }
+                        } else {   // acc + 0.0 == acc (acc >= +0): a select, no branch
+                            const double r0 = res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x, ur[iN].x,
+                                                          uW, ur[iS].x, ur[iR].y, c);
+                            acc += (keep && rin) ? r0 * r0 : 0.0;
+                        }
+                    }
                     load_rv(s + 3, rd[(p + 3) % NR]);
                     if (p & 1) {   // end of a pair (compile-time)
                         __syncthreads();
@@ -1074,41 +1149,31 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         rd[(q + 3) % NR].x = slot[1][l];
                         rd[(q + 3) % NR].y = slot[2][l];
                     }
-                    // residual norm of u_post (multigrid.cpp:112-113) on row s+2:
-                    // rows s+1..s+3 are still untouched u_post here
+                    // residual norm of u_post (multigrid.cpp:112-113) on row s+2,
+                    // column c0+1 (A takes c0): rows s+1..s+3 are still untouched
+                    // u_post here
                     {
                         const int r = s + 2;
                         const int iR = (q + 2) % NR, iN = (q + 1) % NR, iS = (q + 3) % NR;
                         const RowData &d = rd[iR];
-                        const double uW = dpp_shr1(ur[iR].y);
                         const double uE = dpp_shl1(ur[iR].x);
                         const bool rin = r >= a && r < b;
                         if (GN) {
-                            if (rin && keep && r >= 1 && r <= n - 1) {
-                                if (in0) {
-                                    const double res =
-                                        res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x, ur[iN].x,
-                                                    uW, ur[iS].x, ur[iR].y, c);
-                                    acc += res * res;
-                                }
-                                if (in1) {
-                                    const double res =
-                                        res_point_t(d.r.y, d.x.y, d.y.y, ur[iR].y, ur[iN].y,
-                                                    ur[iR].x, ur[iS].y, uE, c);
-                                    acc += res * res;
-                                }
+                            if (rin && keep && r >= 1 && r <= n - 1 && in1) {
+                                const double res =
+                                    res_point_t(d.r.y, d.x.y, d.y.y, ur[iR].y, ur[iN].y,
+                                                ur[iR].x, ur[iS].y, uE, c);
+                                acc += res * res;
                             }
-                        } else {   // acc + 0.0 == acc (acc >= +0): selects, no branch
-                            const double r0 = res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x,
-                                                          ur[iN].x, uW, ur[iS].x, ur[iR].y, c);
+                        } else {   // acc + 0.0 == acc (acc >= +0): a select, no branch
                             const double r1 = res_point_t(d.r.y, d.x.y, d.y.y, ur[iR].y,
                                                           ur[iN].y, ur[iR].x, ur[iS].y, uE, c);
-                            acc += (keep && rin) ? r0 * r0 : 0.0;
                             acc += (keep && rin) ? r1 * r1 : 0.0;
                         }
                     }
+                    to_coef(rd[(q + 1) % NR], cf[(q + 1) % NR]);   // row s+1
 #pragma unroll
-                    for (int h = 0; h < S; ++h) stage(ur, rd, q, h, s + 1 - h);
+                    for (int h = 0; h < S; ++h) stage_c(q, h, s + 1 - h);
                     {
                         const int ro = s + 2 - S;
                         st2_if(upre + (long)ro * pitch, c0, ro >= a && ro < b && keep,
@@ -1120,12 +1185,10 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         const int iR = (q + 1 - S + 2 * NR) % NR;
                         const int iN = (q - S + 2 * NR) % NR;
                         const int iS = (q + 2 - S + 2 * NR) % NR;
-                        const RowData &d = rd[iR];
                         const double uW = dpp_shr1(ur[iR].y);
                         const bool on = r >= a && r < b && keep &&
                                         (!GN || (r >= 1 && r <= n - 2 && in0 && c0 <= n - 2));
-                        const double res = res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x, ur[iN].x,
-                                                       uW, ur[iS].x, ur[iR].y, c);
+                        const double res = res_x(iR, iN, iS, uW);
                         st1_if(rhsc + (long)(r >> 1) * pitchc, c0 >> 1, on, res);
                     }
                     if (p & 1) {
@@ -1147,10 +1210,8 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
         // so each pair's barrier count still matches between its two waves)
         if (__builtin_amdgcn_readfirstlane(strip) >= 0) march(strip * W, a, b);
     }
-    if (!isA) {
-        const double tot = wave_sum(acc);
-        if (l == 0) partials[(long)blockIdx.x * WPB + pr] = tot;
-    }
+    const double tot = wave_sum(acc);   // one partial per wave (A: columns c0, B: c0+1)
+    if (l == 0) partials[(long)blockIdx.x * 2 * WPB + wv] = tot;
 }
 
 // k_smooth_tile: the same fused pass (K sweeps + optional prolong / restrict
@@ -1817,7 +1878,7 @@ static int xsmooth_slots() {
 
 // One launch over `reg`; min_rows: the fewest rows per workgroup (each
 // workgroup's march pays a warm-up of ~EA + EB + D rows).  Returns the norm
-// partials written (grid * WPB) at `partials`.
+// partials written (grid * 2 * WPB: one per wave) at `partials`.
 template <int WPB, int K, bool G>
 static int xsmooth_launch(const XArgs &A, const MarchRegions &reg, double *partials, int lo, int hi,
                           long min_rows, long max_wgs, hipStream_t s) {
@@ -1830,7 +1891,7 @@ static int xsmooth_launch(const XArgs &A, const MarchRegions &reg, double *parti
     MGX_LAUNCH((k_xsmooth<WPB, K, G>), dim3(grid), dim3(128 * WPB), s, A.uin, A.upost, A.upre,
                A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch,
                order_regions(reg, upw), upw, A.c, lo, hi, A.store_post ? 1 : 0);
-    return (int)grid * WPB;
+    return (int)grid * 2 * WPB;
 }
 
 // The cross pass as two launches: the unguarded kernel over the interior
@@ -1857,9 +1918,9 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
     march_regions<WPB>(n, X::W, X::H, ra, rb, X::TOP, X::BOT, split, inner, unused);
     march_regions<1>(n, X::W, X::H, ra, rb, X::TOP, X::BOT, split, unused, edge);
     const int pm = xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, A.min_rows,
-                                                 kNormBlocks / WPB / 2, s);
+                                                 kNormBlocks / (2 * WPB) / 2, s);
     const int pe = xsmooth_launch<1, K, true>(A, edge, A.partials + pm, lo, hi,
-                                              std::min(32, A.min_rows), kNormBlocks / 2, s);
+                                              std::min(32, A.min_rows), kNormBlocks / 2 / 2, s);
     return pm + pe;
 }
 
