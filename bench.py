@@ -120,6 +120,8 @@ def parse():
                          "partitioning the same grid")
     ap.add_argument("--row-upload", choices=["auto", "on", "off"], default="auto",
                     help="multi-GPU: each rank builds only its rows (auto: N > 16384)")
+    ap.add_argument("--rccl-check", type=int, default=1,
+                    help="N > 1: first check libmgx's RCCL path bitwise vs one GPU (N=1024)")
     ap.add_argument("--no-profile", action="store_true",
                     help="do not record per-kernel HIP events in the timed region")
     ap.add_argument("--sweep", nargs=2, type=int, metavar=("NMIN", "NMAX"),
@@ -270,6 +272,13 @@ def main():
     def barrier():
         if world > 1:
             dist.barrier()
+
+    rccl_check = None
+    if world > 1 and args.rccl_check:
+        # libmgx's own RCCL transport with real peers vs a one-GPU context,
+        # bitwise (small problem, before and outside the timed region)
+        from hpcclassmultigridproject_amd import dist as mgdist
+        rccl_check = mgdist.rccl_selfcheck(world, rank, local)
 
     N, L = args.N, args.levels
     if args.weak and world > 1:
@@ -423,6 +432,8 @@ def main():
         "roofline": roof,
         "kernels": kernels,
     }
+    if rccl_check is not None:
+        out["rccl_parity"] = rccl_check
     if rank == 0 and world == 1 and args.cpu_baseline != "off":
         try:
             out["cpu_baseline"] = cpu_baseline(args)

@@ -110,6 +110,10 @@ int launch_xsmooth(const XArgs &a, int sweeps, hipStream_t s);
 // Cross pass: 1 = interior strips run the unguarded march (default), 0 = all guarded.
 void set_xfast(long v);
 long get_xfast();
+// Cross pass on row blocks of <= xtile_max_rows rows (default 8193): edges as
+// LDS tiles instead of the guarded march (0 = never).
+void set_xtile_max_rows(long v);
+long get_xtile_max_rows();
 // Levels with n <= tile_max_n use the 2-D tile form of the fused pass (small
 // levels: latency bound), larger ones the row march.  Default 2048, or the
 // MGX_TILE_MAX_N environment variable.

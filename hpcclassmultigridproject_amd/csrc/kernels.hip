@@ -607,6 +607,10 @@ struct WCfg {
     static constexpr int TOP = E + NR + S + 2, BOT = E + 4;
 };
 
+#ifndef MGX_WRV
+#define MGX_WRV 2
+#endif
+
 // 64-bit value of lane l-1 (shr) / l+1 (shl); the edge lane reads 0
 // (bound_ctrl: one v_mov_b32_dpp per half, no zeroing move)
 __device__ __forceinline__ double dpp_shr1(double v) {
@@ -647,6 +651,10 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
     MarchRegions reg, long units_per_wg, Coef c, int lo, int hi) {
     using C = WCfg<K, MODE>;
     constexpr int S = C::S, E = C::E, H = C::H, NR = C::NR, W = C::W;
+    // rhs/v prefetch distance in steps (row s+WRV takes the slot of row
+    // s+WRV-NR, last used by the residual stage on row s+1-S)
+    constexpr int WRV = MGX_WRV;
+    static_assert(WRV >= 2 && WRV <= NR - S + 1, "rhs/v prefetch distance");
     // WPB waves per workgroup march WPB adjacent strips over the same rows,
     // independently (no barriers); their row loads are adjacent 1-KiB pieces
     // of the same rows, issued at about the same time
@@ -748,8 +756,8 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
         }
         load_u(s + 3, up[1]);
         load_u(s + 4, up[0]);
-        load_rv(s + 1, rd[1]);
-        load_rv(s + 2, rd[2]);
+#pragma unroll
+        for (int d = 1; d < WRV; ++d) load_rv(s + d, rd[d]);
 
         for (;;) {
 #pragma unroll
@@ -833,8 +841,8 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                         }
                     }
                 }
-                // (5) rhs/v row s+3 into the slot of row s+3-NR (dead)
-                load_rv(s + 3, rd[(p + 3) % NR]);
+                // (5) rhs/v row s+WRV into the slot of row s+WRV-NR (dead)
+                load_rv(s + WRV, rd[(p + WRV) % NR]);
                 if (++s > s_last) goto done;
             }
         }
@@ -865,6 +873,12 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
 // which mg_outer returns if cycle k converged); B stores u_pre (cycle k+1
 // after its pre-smoothing).  Exactness: B's output strip needs A's output
 // on a cone EB = S+1 wider, A's on S more: H = ceil((S+EB)/2) halo pairs.
+#ifndef MGX_XRV
+#define MGX_XRV 4
+#endif
+#ifndef MGX_XU
+#define MGX_XU 2
+#endif
 template <int K>
 struct XCfg {
     static constexpr int S = 2 * K;
@@ -906,6 +920,17 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     using X = XCfg<K>;
     constexpr int S = X::S, H = X::H, NR = X::NR, W = X::W, D = X::D, NU = X::NU,
                   NRD = X::NRD, EA = X::EA, EB = X::EB;
+    // A's prefetch distances in steps: rhs/v rows XRV ahead of their first
+    // stage, u rows (+ coarse parents) XU ahead of entering the ring.  The
+    // pass is bound by loads in flight, not by VALU: rhs/v 2 -> 3 -> 4 steps
+    // took level 0 -4 % and -3 % at the same VGPR count (B's path sets it);
+    // u 3-4 steps or rhs/v 5 measured no better (N=16384, tools/ab_libs.sh).
+    constexpr int XRV = MGX_XRV;
+    constexpr int XU = MGX_XU;
+    static_assert(XU >= 1 && XU <= NR - 3, "u prefetch distance");
+    // row s+XRV takes the ring slot of row s+XRV-NR, last used by A's norm of
+    // row s+1-S
+    static_assert(XRV >= 2 && XRV <= NR - S + 1, "rhs/v prefetch distance");
     __shared__ double2 uring[WPB][NU][64];
     // rhs / t1 / t2 planes: each hand-off access is 16 B per lane, unit stride
     __shared__ double2 rdring[WPB][NRD][3][64];
@@ -938,8 +963,10 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             double2 X;
             double q00, q01, q10, q11;
         };
-        UPre up[2];
-        up[0] = up[1] = UPre{make_double2(0.0, 0.0), 0.0, 0.0, 0.0, 0.0};
+        // u rows + coarse parents in flight, a ring by row like rd
+        UPre up[NR];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) up[i] = UPre{make_double2(0.0, 0.0), 0.0, 0.0, 0.0, 0.0};
         auto load_u = [&](int R, UPre &u) {   // A: u row R + its coarse parents
             const int Rc = min(max(R, lo), hi);
             u.X = ld2((uin + (long)Rc * pitch) + cl);
@@ -1072,19 +1099,19 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
         if (isA) {
 #pragma unroll
             for (int d = 0; d < 3; ++d) {
-                load_u(s0 + d, up[0]);
-                ur[d] = make_u(s0 + d, up[0], d & 1);
+                load_u(s0 + d, up[d]);
+                ur[d] = make_u(s0 + d, up[d], d & 1);
             }
-            load_u(s0 + 3, up[1]);
-            load_u(s0 + 4, up[0]);
-            load_rv(s0 + 1, rd[1]);
-            load_rv(s0 + 2, rd[2]);
+#pragma unroll
+            for (int d = 3; d < 3 + XU; ++d) load_u(s0 + d, up[d]);
+#pragma unroll
+            for (int d = 1; d < XRV; ++d) load_rv(s0 + d, rd[d]);
             for (;;) {
 #pragma unroll
                 for (int p = 0; p < NR; ++p) {   // s == p (mod NR)
                     const int s = s0 + it + (p & 1);
-                    ur[(p + 3) % NR] = make_u(s + 3, up[(p + 1) & 1], (p + 3) & 1);
-                    load_u(s + 5, up[(p + 1) & 1]);
+                    ur[(p + 3) % NR] = make_u(s + 3, up[(p + 3) % NR], (p + 3) & 1);
+                    load_u(s + 3 + XU, up[(p + 3 + XU) % NR]);   // XU steps ahead
 #pragma unroll
                     for (int h = 0; h < S; ++h) stage(ur, rd, p, h, s + 1 - h);
                     // hand-off: rhs/v row s+1 (first used above), final u row s+2-S
@@ -1125,7 +1152,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                             acc += (keep && rin) ? r0 * r0 : 0.0;
                         }
                     }
-                    load_rv(s + 3, rd[(p + 3) % NR]);
+                    load_rv(s + XRV, rd[(p + XRV) % NR]);
                     if (p & 1) {   // end of a pair (compile-time)
                         __syncthreads();
                         it += 2;
@@ -1387,6 +1414,232 @@ __global__ __launch_bounds__(256) void k_smooth_tile(
         const double tot = block_sum(acc, red_lds);
         if (t == 0) partials[bid] = tot;
     }
+}
+
+// k_xtile: the cross-cycle pass of k_xsmooth as 2-D LDS tiles, for the edge
+// regions of a SHORT row block (a multi-GPU rank's two boundary strips and
+// its top / bottom bands) and for short row ranges (the bands of the
+// overlapped exchange).  There the guarded row march is latency bound: every
+// workgroup pays a ~40-row warm-up on a short segment, one dependent row step
+// after another (~0.15 ms whatever the block height), while a tile runs all
+// its stages on all its rows at once (the cost grows with the rows instead:
+// on a whole 16384-row level the march stays faster).
+//
+// A workgroup owns a TR x 64 output tile and loads it with an EH-point halo
+// (EH = E rounded up to even, E = the stages of the pass plus its residual
+// stage) into LDS, split by colour: point (r, col) of the extended tile lives
+// in plane (r + col) & 1 at index r*HW + col/2, so a stage's own points and
+// all four neighbours are consecutive 8-B words across consecutive lanes (no
+// bank conflicts).  Stages run as parallel colour updates with one barrier
+// between them; the exact region shrinks by one point per stage, so the
+// owned points are exact (EH >= E).
+//
+// Thread map: threads 0..127 own column pairs of the even rows, 128..255 of
+// the odd rows, so in every stage each thread updates the same point of each
+// of its pairs (x = column 2k on even-parity stages of even rows, ...) and
+// all its operands sit at compile-time indices: each pair keeps the rhs and
+// the four coefficients (gs.cpp:126-129) of its two points, computed once
+// from v1 / v2 at load instead of in every stage.  The same expressions as
+// gs_point, so every value is bitwise the reference's.
+//
+// The pass: S stages of the post-smoothing of cycle k from uin + P(uc)
+// (gs.cpp:238-265), the residual norm of u_post (multigrid.cpp:112-113, one
+// partial per tile) and the optional u_post store, S stages of the
+// pre-smoothing of cycle k+1, the u_pre store and the residual at the
+// even-even points -> coarse rhs (multigrid.cpp:73-75).
+// Owned regions: up to 4 rectangles of columns [c0, c1) x rows [r0, r1),
+// each cut into TR x 64 tiles from (r0 & ~1, c0 & ~1) (even tile origins:
+// the planes are the global colours); a tile owns its points inside its
+// rectangle.
+struct TileRegions {
+    int c0[4], c1[4], r0[4], r1[4];
+    int tx[4];     // tiles per tile row of region k
+    int pre[5];    // prefix tile counts
+    int count;
+};
+
+template <int K, int TRV>
+struct XTileCfg {
+    static constexpr int S = 2 * K;
+    static constexpr int E = 2 * S + 1;   // both halves + the restriction residual
+    static constexpr int EH = (E + 1) / 2 * 2;
+    static constexpr int TR = TRV, TC = 64;
+    static constexpr int RT = TR + 2 * EH, WT = TC + 2 * EH, HW = WT / 2;
+    static constexpr int PL = RT * HW;              // plane size (doubles)
+    static constexpr int HALF = (RT / 2) * HW;      // pairs of one row parity
+    static constexpr int PPT = (HALF + 127) / 128;  // pairs per thread
+};
+
+// rhs and coefficients of one point: (rhs - cn*uN - cw*uW - cs*uS - ce*uE) / d
+struct PtCoef {
+    double f, cn, cw, cs, ce;
+};
+
+template <int K, int TRV>
+__global__ __launch_bounds__(256) void k_xtile(
+    const double *__restrict__ uin, double *__restrict__ uout, double *__restrict__ upost,
+    const double *__restrict__ rhs, const double *__restrict__ v1, const double *__restrict__ v2,
+    const double *__restrict__ uc, long pitchc, double *__restrict__ rhsc,
+    double *__restrict__ partials, int n, long pitch, TileRegions reg, Coef c, int lo, int hi,
+    int store_post) {
+    using T = XTileCfg<K, TRV>;
+    constexpr int S = T::S, EH = T::EH, WT = T::WT, RT = T::RT, PPT = T::PPT, HW = T::HW;
+    constexpr int PL = T::PL, HALF = T::HALF;
+    __shared__ __attribute__((aligned(16))) double tu[2 * PL];
+    __shared__ double red_lds[4];
+
+    const int t = threadIdx.x;
+    const int bid = blockIdx.x;
+    int k = 0;
+    while (k + 1 < reg.count && bid >= reg.pre[k + 1]) ++k;
+    const int loc = bid - reg.pre[k];
+    const int ty = loc / reg.tx[k], tx = loc % reg.tx[k];
+    const int R0 = (reg.r0[k] & ~1) + ty * T::TR, C0 = (reg.c0[k] & ~1) + tx * T::TC;
+    const int oa = max(R0, reg.r0[k]), ob = min(R0 + T::TR, reg.r1[k]);   // owned rows
+    const int ca = max(C0, reg.c0[k]), cb = min(C0 + T::TC, reg.c1[k]);   // owned columns
+    const long i0 = R0 - EH, j0 = C0 - EH;   // tile origin (even, even)
+    const int nc = n >> 1;
+    const int par = t >> 7;   // row parity of this thread's pairs (wave-uniform)
+    const int u = t & 127;
+
+    // pair m: LDS index q[m]; P0[m] = the point updated on even stages (column
+    // 2k + par), P1[m] the other; bits: 2m / 2m+1 updatable, 2m+... owned
+    int qi[PPT];
+    PtCoef P0[PPT], P1[PPT];
+    unsigned upd = 0, own = 0;
+#pragma unroll
+    for (int m = 0; m < PPT; ++m) {
+        const int j = u + m * 128;
+        qi[m] = 0;
+        P0[m] = P1[m] = PtCoef{0.0, 0.0, 0.0, 0.0, 0.0};
+        if (j >= HALF) continue;
+        const int r = 2 * (j / HW) + par, kk = j % HW;
+        const int q = r * HW + kk;
+        qi[m] = q;
+        const long gi = i0 + r, gj = j0 + 2 * kk;
+        double2 v = make_double2(0.0, 0.0);
+        if (gi >= lo && gi <= hi && gj >= 0 && gj <= n) {
+            const long o = gi * pitch + gj;
+            v = ld2(uin + o);
+            {
+                const long ii = gi >> 1, jj = gj >> 1;
+                const double *p0 = uc + ii * pitchc + jj;
+                const double q00 = p0[0], q01 = (jj + 1 <= nc) ? p0[1] : 0.0;
+                double2 pr;
+                if (!(gi & 1)) {
+                    pr.x = q00;
+                    pr.y = (q00 + q01) / 2;
+                } else {
+                    const double q10 = p0[pitchc], q11 = (jj + 1 <= nc) ? p0[pitchc + 1] : 0.0;
+                    pr.x = (q00 + q10) / 2;
+                    pr.y = (q00 + q10 + q01 + q11) / 4;
+                }
+                v.x = v.x + pr.x;
+                v.y = v.y + pr.y;
+            }
+            const double2 rr = ld2(rhs + o), xx = ld2(v1 + o), yy = ld2(v2 + o);
+            // gs.cpp:126-129: aa, bb from v2 (W / E), cc, dd from v1 (N / S)
+            const PtCoef X{rr.x, coef_a(xx.x, c), coef_a(yy.x, c), coef_b(xx.x, c), coef_b(yy.x, c)};
+            const PtCoef Y{rr.y, coef_a(xx.y, c), coef_a(yy.y, c), coef_b(xx.y, c), coef_b(yy.y, c)};
+            P0[m] = par ? Y : X;
+            P1[m] = par ? X : Y;
+#pragma unroll
+            for (int cs = 0; cs < 2; ++cs) {   // cs: column 2kk + cs
+                if (gi >= 1 && gi <= n - 1 && gj + cs >= 1 && gj + cs <= n - 1 && r >= 1 &&
+                    r <= RT - 2 && 2 * kk + cs >= 1 && 2 * kk + cs <= WT - 2)
+                    upd |= 1u << (2 * m + (cs ^ par));   // bit 2m: even stages
+            }
+            if (gi >= oa && gi < ob && gj >= ca && gj < cb) own |= 1u << m;
+        }
+        tu[par * PL + q] = v.x;          // column 2kk: plane r & 1 = par
+        tu[(par ^ 1) * PL + q] = v.y;
+    }
+    __syncthreads();
+
+    // stages [h0, h1): stage h updates plane h & 1; this thread's point of
+    // pair m there is column 2k + cs, cs = par ^ (h & 1): W = q-1+cs, E = q+cs
+    auto stages = [&](const int h0, const int h1) {
+#pragma unroll
+        for (int h = h0; h < h1; ++h) {
+            const int cs = par ^ (h & 1);
+            double *ow = tu + (h & 1) * PL;
+            const double *ot = tu + ((h & 1) ^ 1) * PL;
+#pragma unroll
+            for (int m = 0; m < PPT; ++m) {
+                if (!((upd >> (2 * m + (h & 1))) & 1u)) continue;
+                const int q = qi[m];
+                const PtCoef &P = (h & 1) ? P1[m] : P0[m];
+                const double uN = ot[q - HW], uS = ot[q + HW];
+                const double uW = ot[q - 1 + cs], uE = ot[q + cs];
+                ow[q] = div_diag(P.f - P.cn * uN - P.cw * uW - P.cs * uS - P.ce * uE, c);
+            }
+            __syncthreads();
+        }
+    };
+    // residual of this thread's point (even-stage point e = 1: P0, else P1) of pair m
+    auto residual = [&](const int m, const bool even_pt) -> double {
+        const int q = qi[m];
+        const int cs = even_pt ? par : par ^ 1;      // column 2k + cs
+        const int pl = even_pt ? 0 : 1;              // its plane
+        const double *pu = tu + pl * PL, *ot = tu + (pl ^ 1) * PL;
+        const PtCoef &P = even_pt ? P0[m] : P1[m];
+        // gs.cpp:75: rhs - (d*u + cc*uN + aa*uW + dd*uS + bb*uE)
+        return P.f - (c.dgs * pu[q] + P.cn * ot[q - HW] + P.cw * ot[q - 1 + cs] +
+                      P.cs * ot[q + HW] + P.ce * ot[q + cs]);
+    };
+    auto gidx = [&](const int m, long &gi, long &gj) {
+        const int r = qi[m] / HW, kk = qi[m] % HW;
+        gi = i0 + r;
+        gj = j0 + 2 * kk;
+    };
+    // owned pairs -> dst (column 2k lives in plane par, 2k+1 in the other)
+    auto store = [&](double *dst) {
+#pragma unroll
+        for (int m = 0; m < PPT; ++m) {
+            if (!((own >> m) & 1u)) continue;
+            long gi, gj;
+            gidx(m, gi, gj);
+            const int q = qi[m];
+            st2(dst + gi * pitch + gj, make_double2(tu[par * PL + q], tu[(par ^ 1) * PL + q]));
+        }
+    };
+    // sum of squares of the residual over the owned interior points
+    auto norm_acc = [&]() -> double {
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < PPT; ++m) {
+            if (!((own >> m) & 1u)) continue;
+            long gi, gj;
+            gidx(m, gi, gj);
+            if (gi < 1 || gi > n - 1) continue;
+            // the even-stage point (column 2k + par), then the other; static
+            // operand indices (a runtime choice would put P0 / P1 in scratch)
+            const bool okx = gj >= 1 && gj <= n - 1, oky = gj + 1 <= n - 1;
+            const double re = residual(m, true), ro = residual(m, false);
+            acc += (par ? oky : okx) ? re * re : 0.0;
+            acc += (par ? okx : oky) ? ro * ro : 0.0;
+        }
+        return acc;
+    };
+
+    stages(0, S);   // post-smoothing of cycle k
+    if (store_post) store(upost);
+    const double acc = norm_acc();
+    __syncthreads();
+    stages(S, 2 * S);   // pre-smoothing of cycle k+1
+    store(uout);
+    if (par == 0) {   // even rows: residual -> coarse rhs at the even-even points
+#pragma unroll
+        for (int m = 0; m < PPT; ++m) {
+            if (!((own >> m) & 1u)) continue;
+            long gi, gj;
+            gidx(m, gi, gj);
+            if (gi < 1 || gi > n - 2 || gj < 1 || gj > n - 2) continue;
+            rhsc[(gi >> 1) * pitchc + (gj >> 1)] = residual(m, true);   // column 2k
+        }
+    }
+    const double tot = block_sum(acc, red_lds);
+    if (t == 0) partials[bid] = tot;
 }
 
 // One colour in place (two launches = one sweep).  Grid (strips, interior rows).
@@ -1767,13 +2020,13 @@ static void add_region(MarchRegions &r, int sfirst, int slim, int r0, int r1) {
 // the unguarded kernel's work -- interior strips (every lane a column in
 // [1, n-1]) x rows [TOP, n+1-BOT) -- and the guarded kernel's: the boundary
 // strips and the top / bottom bands (~1-2 % of the points).
-template <int WPB>
-static void march_regions(long n, int W, int H, int ra, int rb, int top, int bot, bool split,
-                          MarchRegions &inner, MarchRegions &edge) {
-    inner = MarchRegions{};
-    edge = MarchRegions{};
+// interior strips [si0, si1) (every lane a column in [1, n-1]) and the rows
+// [ma, mb) of [ra, rb) an unguarded march may own
+static void march_split(long n, int W, int H, int ra, int rb, int top, int bot, int &si0,
+                        int &si1, int &ma, int &mb) {
     const int strips = (int)((n + 1 + W - 1) / W);
-    int si0 = strips, si1 = 0;   // interior strips [si0, si1)
+    si0 = strips;
+    si1 = 0;
     for (int st = 0; st < strips; ++st) {
         const long c_first = (long)st * W - 2 * H, c_last = c_first + 127;
         if (c_first >= 1 && c_last <= n - 1) {
@@ -1781,7 +2034,18 @@ static void march_regions(long n, int W, int H, int ra, int rb, int top, int bot
             si1 = st + 1;
         }
     }
-    const int ma = std::max(ra, top), mb = std::min(rb, (int)n + 1 - bot);
+    ma = std::max(ra, top);
+    mb = std::min(rb, (int)n + 1 - bot);
+}
+
+template <int WPB>
+static void march_regions(long n, int W, int H, int ra, int rb, int top, int bot, bool split,
+                          MarchRegions &inner, MarchRegions &edge) {
+    inner = MarchRegions{};
+    edge = MarchRegions{};
+    const int strips = (int)((n + 1 + W - 1) / W);
+    int si0, si1, ma, mb;
+    march_split(n, W, H, ra, rb, top, bot, si0, si1, ma, mb);
     if (split && si1 > si0 && mb > ma) {
         add_region<WPB>(inner, si0, si1, ma, mb);
         add_region<WPB>(edge, 0, si0, ra, rb);
@@ -1894,6 +2158,61 @@ static int xsmooth_launch(const XArgs &A, const MarchRegions &reg, double *parti
     return (int)grid * 2 * WPB;
 }
 
+static void add_tile_region(TileRegions &r, int c0, int c1, int r0, int r1, int TR) {
+    if (c1 <= c0 || r1 <= r0) return;
+    const int k = r.count++;
+    r.c0[k] = c0;
+    r.c1[k] = c1;
+    r.r0[k] = r0;
+    r.r1[k] = r1;
+    r.tx[k] = (c1 - (c0 & ~1) + 63) / 64;
+    const int ty = (r1 - (r0 & ~1) + TR - 1) / TR;
+    r.pre[k + 1] = r.pre[k] + r.tx[k] * ty;
+}
+
+// Row blocks of at most this many rows run the cross pass's edges as tiles
+// (tuning key "xtile_max_rows"; 0 = never); row ranges too short for the
+// unguarded march (< kXTileAllRows rows between its margins) run entirely as
+// tiles.
+long g_xtile_max_rows = 8193;
+void set_xtile_max_rows(long v) { g_xtile_max_rows = v; }
+long get_xtile_max_rows() { return g_xtile_max_rows; }
+constexpr int kXTileAllRows = 96;
+constexpr int kXTileRows = 16;
+
+// The cross pass of a short row block: the unguarded march over the interior
+// strips x rows [ma, mb), k_xtile over the boundary strips and the top /
+// bottom bands (or over everything, when [ma, mb) is short).
+template <int WPB, int K>
+static int xsmooth_tiled(const XArgs &A, int ra, int rb, int lo, int hi, hipStream_t s) {
+    using X = XCfg<K>;
+    const long n = A.n;
+    int si0, si1, ma, mb;
+    march_split(n, X::W, X::H, ra, rb, X::TOP, X::BOT, si0, si1, ma, mb);
+    TileRegions t{};
+    int pm = 0;
+    if (si1 > si0 && mb - ma >= kXTileAllRows) {
+        MarchRegions inner{};
+        add_region<WPB>(inner, si0, si1, ma, mb);
+        pm = xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, A.min_rows,
+                                           kNormBlocks / (2 * WPB) / 2, s);
+        const int ca = si0 * X::W, cb = (int)std::min<long>(n + 1, (long)si1 * X::W);
+        add_tile_region(t, 0, ca, ra, rb, kXTileRows);
+        add_tile_region(t, cb, (int)n + 1, ra, rb, kXTileRows);
+        add_tile_region(t, ca, cb, ra, ma, kXTileRows);
+        add_tile_region(t, ca, cb, mb, rb, kXTileRows);
+    } else {
+        add_tile_region(t, 0, (int)n + 1, ra, rb, kXTileRows);
+    }
+    const int tiles = t.pre[t.count];
+    if (pm + tiles > kNormBlocks) return -1;
+    if (tiles > 0)
+        MGX_LAUNCH((k_xtile<K, kXTileRows>), dim3((unsigned)tiles), dim3(256), s, A.uin, A.upre,
+                   A.upost, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, A.partials + pm, (int)n,
+                   A.pitch, t, A.c, lo, hi, A.store_post ? 1 : 0);
+    return pm + tiles;
+}
+
 // The cross pass as two launches: the unguarded kernel over the interior
 // strips x rows [TOP, n+1-BOT), the guarded one over the rest (boundary
 // strips, top / bottom bands: ~1.7 % of the points at N=16384).
@@ -1915,6 +2234,7 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
     MarchRegions inner, edge, unused;
     // the unguarded kernel's division assumes d > 0 (div_diag<true>)
     const bool split = g_xfast != 0 && A.c.dgs > 0;
+    if (split && rb - ra <= g_xtile_max_rows) return xsmooth_tiled<WPB, K>(A, ra, rb, lo, hi, s);
     march_regions<WPB>(n, X::W, X::H, ra, rb, X::TOP, X::BOT, split, inner, unused);
     march_regions<1>(n, X::W, X::H, ra, rb, X::TOP, X::BOT, split, unused, edge);
     const int pm = xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, A.min_rows,

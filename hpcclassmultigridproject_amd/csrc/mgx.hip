@@ -968,6 +968,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgx::set_march_min_rows(value);
         return MGX_OK;
     }
+    if (!strcmp(key, "xtile_max_rows")) {
+        if (value < 0) return fail(MGX_E_ARG, "xtile_max_rows must be >= 0");
+        mgx::set_xtile_max_rows(value);
+        return MGX_OK;
+    }
     if (!strcmp(key, "coarse_lds")) {
         if (value != 0 && value != 1) return fail(MGX_E_ARG, "coarse_lds must be 0 or 1");
         mgx::set_coarse_lds(value);
@@ -1012,6 +1017,10 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "march_min_rows")) {
         *value = mgx::get_march_min_rows();
+        return MGX_OK;
+    }
+    if (!strcmp(key, "xtile_max_rows")) {
+        *value = mgx::get_xtile_max_rows();
         return MGX_OK;
     }
     if (!strcmp(key, "coarse_lds")) {

@@ -75,3 +75,62 @@ def gather_plan(n: int, maxlvl: int, world: int, rank: int):
     check(lib().mgx_gather_plan(n, maxlvl, world, rank, C.byref(lv), C.byref(r0),
                                 C.byref(rows)))
     return lv.value, r0.value, rows.value
+
+
+def rccl_selfcheck(world: int, rank: int, device: int, n: int = 1024, maxlvl: int = 6,
+                   cycles: int = 2, group=None) -> dict:
+    """Run libmgx's RCCL transport with real peers against a single-GPU context.
+
+    Every rank builds a row-partitioned context of the same small problem
+    (``dist_min_rows`` 16, so levels 0..3 are split even at world 8) and runs
+    ``cycles`` V-cycles with the cross-cycle pass -- ghost send/recv, the
+    all-gather into the replicated levels, the norm all-reduce, the
+    all-gather + broadcast of the download -- once with the exchanges on the
+    compute stream and once overlapped (``dist_overlap``); rank 0 compares u
+    bitwise and the norms to 1e-11 with a one-GPU context.  Collective over
+    the torch.distributed group (its backend only brokers the unique ids and
+    the verdict).  -> {"bitwise": bool, "norm_rel_err": float, ...} on every rank.
+    """
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from .multigrid import Multigrid, init_problem
+
+    dt, nu = 1.0 / n / 10, -4e-4
+    u0, v1, v2 = init_problem(n)
+    old_rows, old_ov = _lib.get_tuning("dist_min_rows"), _lib.get_tuning("dist_overlap")
+    ref = None
+    if rank == 0:
+        with Multigrid(n, maxlvl, dt, nu, device=device) as mg:
+            mg.upload(u0, v1, v2)
+            mg.rhs()
+            ref = ([mg.run_cycles(1) for _ in range(cycles)], mg.download())
+    ok, err, la = True, 0.0, None
+    try:
+        _lib.set_tuning("dist_min_rows", 16)
+        for ov in (0, 1):
+            _lib.set_tuning("dist_overlap", ov)
+            uid = broadcast_unique_id(group)
+            with Multigrid(n, maxlvl, dt, nu, device=device, world=world, rank=rank,
+                           unique_id=uid) as mg:
+                la = mg.dist_info()[2]
+                mg.upload(u0, v1, v2)
+                mg.rhs()
+                norms = [mg.run_cycles(1) for _ in range(cycles)]
+                u = mg.download()
+            if rank == 0:
+                ok = ok and bool(np.array_equal(u, ref[1]))
+                err = max(err, float(np.max(np.abs(np.array(norms) - ref[0]) /
+                                            np.abs(ref[0]))))
+    finally:
+        _lib.set_tuning("dist_min_rows", old_rows)
+        _lib.set_tuning("dist_overlap", old_ov)
+    verdict = torch.tensor([1.0 if ok else 0.0, err], dtype=torch.float64)
+    if dist.get_backend(group) == "nccl":
+        verdict = verdict.cuda()
+    dist.broadcast(verdict, src=0, group=group)
+    ok, err = bool(verdict[0].item() == 1.0), float(verdict[1].item())
+    return {"N": n, "levels": maxlvl, "cycles": cycles, "partitioned_levels": la,
+            "overlap": [0, 1], "bitwise": ok, "norm_rel_err": err,
+            "passed": ok and err <= 1e-11}

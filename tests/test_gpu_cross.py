@@ -103,25 +103,53 @@ def _cycles_plain(N, L, n, **kw):
         return mg.download(), norms
 
 
-@pytest.mark.parametrize("N,L,G", [(4096, 6, 1), (8192, 5, 1), (4096, 6, 4)],
-                         ids=["N4096", "N8192", "N4096_G4"])
-def test_unguarded_interior_kernel_equals_guarded(N, L, G, cross):
+@pytest.mark.parametrize("xt", [0, 8193], ids=["edge_march", "edge_tiles"])
+@pytest.mark.parametrize("N,L,G", [(4096, 6, 1), (8192, 5, 1), (4096, 6, 4), (4096, 6, 8)],
+                         ids=["N4096", "N8192", "N4096_G4", "N4096_G8"])
+def test_unguarded_interior_kernel_equals_guarded(N, L, G, xt, cross, knobs):
     """Tuning key "xfast": 1 = the cross pass runs as the unguarded interior
-    kernel + the guarded edge kernel, 0 = one guarded launch over the level.
-    u bitwise, norms to the summation-order tolerance; also on row blocks
-    (virtual ranks, whose bands sit only at the first / last block)."""
+    kernel + the edges (boundary strips, top / bottom bands) as the guarded
+    march ("xtile_max_rows" 0) or as LDS tiles (k_xtile, row blocks up to
+    8193 rows); 0 = one guarded launch over the level.  u bitwise, norms to
+    the summation-order tolerance; also on row blocks (virtual ranks, whose
+    bands sit only at the first / last block; at G=8 the 512-row blocks are
+    short enough to run entirely as tiles)."""
     cross(1)
-    old = _lib.get_tuning("xfast")
     kw = dict(local_parts=G) if G > 1 else {}
-    try:
-        _lib.set_tuning("xfast", 0)
-        u0_, n0 = _cycles_plain(N, L, 3, **kw)
-        _lib.set_tuning("xfast", 1)
-        u1_, n1 = _cycles_plain(N, L, 3, **kw)
-    finally:
-        _lib.set_tuning("xfast", old)
+    knobs(xfast=0)
+    u0_, n0 = _cycles_plain(N, L, 3, **kw)
+    knobs(xfast=1, xtile_max_rows=xt)
+    u1_, n1 = _cycles_plain(N, L, 3, **kw)
     assert np.array_equal(u0_, u1_)
     np.testing.assert_allclose(n1, n0, rtol=NORM_RTOL)
+
+
+@pytest.mark.parametrize("store_post", [False, True], ids=["pre_only", "post_too"])
+def test_edge_tiles_store_post_vs_checker(store_post, cross, knobs, oracle_mod):
+    """The edge tiles also write u_post when the cycle's solution is observed
+    (single run_cycles calls; a batch writes only the last): two cycles,
+    bitwise vs the checker's mg_inner."""
+    cross(1)
+    knobs(xfast=1, xtile_max_rows=8193)
+    N, L = 4096, 5
+    dt = 1.0 / N / 10
+    u0, v1, v2 = init_problem(N)
+    with Multigrid(N, L, dt, NU) as mg:
+        mg.upload(u0, v1, v2)
+        mg.rhs()
+        if store_post:
+            mg.run_cycles(1)
+            mg.run_cycles(1)
+        else:
+            mg.run_cycles(2)
+        u = mg.download()
+    O = oracle_mod
+    O.set_threads(8)
+    t = O.Tower(u0, v1, v2, N, L)
+    O.compute_rhs(t.ufine, N, v1, v2, dt, NU, 1.0 / N, rhs=t.rhsfine)
+    for _ in range(2):
+        t.mg_inner(dt, NU)
+    assert np.array_equal(u, t.ufine)
 
 
 @pytest.fixture
