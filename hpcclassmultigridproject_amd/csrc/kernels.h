@@ -110,7 +110,7 @@ int launch_xsmooth(const XArgs &a, int sweeps, hipStream_t s);
 // Cross pass: 1 = interior strips run the unguarded march (default), 0 = all guarded.
 void set_xfast(long v);
 long get_xfast();
-// Cross pass on row blocks of <= xtile_max_rows rows (default 8193): edges as
+// Cross pass on row blocks of <= xtile_max_rows rows (default 4097): edges as
 // LDS tiles instead of the guarded march (0 = never).
 void set_xtile_max_rows(long v);
 long get_xtile_max_rows();

@@ -2174,7 +2174,7 @@ static void add_tile_region(TileRegions &r, int c0, int c1, int r0, int r1, int 
 // (tuning key "xtile_max_rows"; 0 = never); row ranges too short for the
 // unguarded march (< kXTileAllRows rows between its margins) run entirely as
 // tiles.
-long g_xtile_max_rows = 8193;
+long g_xtile_max_rows = 4097;
 void set_xtile_max_rows(long v) { g_xtile_max_rows = v; }
 long get_xtile_max_rows() { return g_xtile_max_rows; }
 constexpr int kXTileAllRows = 96;

@@ -178,7 +178,7 @@ int mgx_synchronize(mgx_ctx *ctx);
  * "xtile_max_rows": on row blocks of at most this many rows (a rank of a
  * partitioned solver, a small level) the cross-cycle pass runs the boundary
  * strips and bands as LDS tiles instead of the guarded row march (latency
- * bound: ~0.15 ms whatever the block height); default 8193, 0 = never.
+ * bound: ~0.15 ms whatever the block height); default 4097, 0 = never.
  * "march_order": work order of the row marches, bit 0 = band-major (the
  * workgroups of neighbouring strip groups march the same rows at the same
  * time, so their shared halo columns are fetched once; launches with >= 192
