@@ -2190,12 +2190,8 @@ static int xsmooth_tiled(const XArgs &A, int ra, int rb, int lo, int hi, hipStre
     int si0, si1, ma, mb;
     march_split(n, X::W, X::H, ra, rb, X::TOP, X::BOT, si0, si1, ma, mb);
     TileRegions t{};
-    int pm = 0;
-    if (si1 > si0 && mb - ma >= kXTileAllRows) {
-        MarchRegions inner{};
-        add_region<WPB>(inner, si0, si1, ma, mb);
-        pm = xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, A.min_rows,
-                                           kNormBlocks / (2 * WPB) / 2, s);
+    const bool inner_march = si1 > si0 && mb - ma >= kXTileAllRows;
+    if (inner_march) {
         const int ca = si0 * X::W, cb = (int)std::min<long>(n + 1, (long)si1 * X::W);
         add_tile_region(t, 0, ca, ra, rb, kXTileRows);
         add_tile_region(t, cb, (int)n + 1, ra, rb, kXTileRows);
@@ -2205,7 +2201,15 @@ static int xsmooth_tiled(const XArgs &A, int ra, int rb, int lo, int hi, hipStre
         add_tile_region(t, 0, (int)n + 1, ra, rb, kXTileRows);
     }
     const int tiles = t.pre[t.count];
-    if (pm + tiles > kNormBlocks) return -1;
+    // one norm partial per tile; the inner march writes at most kNormBlocks / 2
+    if (tiles > kNormBlocks / 2) return -2;   // too many: the caller marches the edges
+    int pm = 0;
+    if (inner_march) {
+        MarchRegions inner{};
+        add_region<WPB>(inner, si0, si1, ma, mb);
+        pm = xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, A.min_rows,
+                                           kNormBlocks / (2 * WPB) / 2, s);
+    }
     if (tiles > 0)
         MGX_LAUNCH((k_xtile<K, kXTileRows>), dim3((unsigned)tiles), dim3(256), s, A.uin, A.upre,
                    A.upost, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, A.partials + pm, (int)n,
@@ -2234,7 +2238,10 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
     MarchRegions inner, edge, unused;
     // the unguarded kernel's division assumes d > 0 (div_diag<true>)
     const bool split = g_xfast != 0 && A.c.dgs > 0;
-    if (split && rb - ra <= g_xtile_max_rows) return xsmooth_tiled<WPB, K>(A, ra, rb, lo, hi, s);
+    if (split && rb - ra <= g_xtile_max_rows) {
+        const int r = xsmooth_tiled<WPB, K>(A, ra, rb, lo, hi, s);
+        if (r != -2) return r;
+    }
     march_regions<WPB>(n, X::W, X::H, ra, rb, X::TOP, X::BOT, split, inner, unused);
     march_regions<1>(n, X::W, X::H, ra, rb, X::TOP, X::BOT, split, unused, edge);
     const int pm = xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, A.min_rows,
