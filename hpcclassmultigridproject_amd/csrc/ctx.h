@@ -129,6 +129,7 @@ int dist_upload(mgx_ctx *c, const double *u0, const double *v1, const double *v2
                 hipMemcpyKind kind);
 int dist_download(mgx_ctx *c, double *u, hipMemcpyKind kind);
 int dist_rhs(mgx_ctx *c);
+int dist_rhs_norm(mgx_ctx *c, double *res0);
 int dist_vcycle(mgx_ctx *c, double *norm, bool store_post = true);
 int dist_residual_norm(mgx_ctx *c, double *norm);
 void dist_free(mgx_ctx *c);

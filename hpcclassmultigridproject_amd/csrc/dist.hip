@@ -595,6 +595,29 @@ int dist_rhs(mgx_ctx *c) {
     return exchange(c, 0, kRhs);
 }
 
+// compute_rhs + the initial residual norm of mg_outer in one pass per part
+// (mgx.hip:op_rhs_norm): u ghosts once, the rhs ghosts after
+int dist_rhs_norm(mgx_ctx *c, double *res0) {
+    Dist *d = c->dist;
+    HIPCHK(hipSetDevice(c->device));
+    dist_drop_spec(c);
+    if (d->la == 0) {
+        CHK(dist_rhs(c));
+        return dist_residual_norm(c, res0);
+    }
+    CHK(exchange(c, 0, kU));
+    for (auto &p : d->parts) {
+        PLevel &L = p.lv[0];
+        CHK(launch(c, MGX_K_RHS, 0, 80.0 * L.Mown(), 32.0 * L.Mown(), [&] {
+            mgx::launch_rhs_norm(L.F(L.rhs), L.U(), L.F(L.v1), L.F(L.v2), L.n, L.pitch, L.coef,
+                                 c->partials, p.dsum, c->stream, L.ra, L.rb,
+                                 /*take_sqrt=*/false);
+        }));
+    }
+    CHK(exchange(c, 0, kRhs));
+    return reduce_norm(c, res0);
+}
+
 int dist_nsub(mgx_ctx *c) { return c->dist ? (int)c->dist->parts.size() : 0; }
 mgx_ctx *dist_sub(mgx_ctx *c, int i) { return c->dist->parts[i].sub; }
 int dist_la(mgx_ctx *c) { return c->dist ? c->dist->la : c->L; }

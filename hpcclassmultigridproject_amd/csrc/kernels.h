@@ -158,6 +158,11 @@ void launch_prolong_add(double *uf, long pitchf, const double *uc, long pitchc, 
                         hipStream_t s);
 void launch_rhs(double *rhs, const double *u, const double *v1, const double *v2, long n,
                 long pitch, Coef c, hipStream_t s, int ra = 0, int rb = -1);
+// compute_rhs stored AND the residual norm against it (rows [ra, rb)), one
+// pass; the norm is bitwise launch_residual_norm's on the new rhs.
+void launch_rhs_norm(double *rhs, const double *u, const double *v1, const double *v2, long n,
+                     long pitch, Coef c, double *partials, double *out, hipStream_t s,
+                     int ra = 0, int rb = -1, bool take_sqrt = true);
 // Coarsest-level solve in one workgroup: repeat {GS; residual; norm} while
 // norm > tol and it < maxit (multigrid.cpp:58-65), in place on u.
 // zero_first: u = 0 before the first sweep.  stats[0] += iterations,

@@ -1657,7 +1657,11 @@ __global__ __launch_bounds__(BLOCK) void k_gs_colour(double *u, const double *rh
 }
 
 // Row march for residual-type kernels.  MODE 0: sum of squares only; MODE 1:
-// residual stored; MODE 2: compute_rhs stored.  Block = 256 lanes = 512 cols,
+// residual stored; MODE 2: compute_rhs stored; MODE 3: compute_rhs stored AND
+// the sum of squares of the residual against it (a time step's rhs and
+// mg_outer's initial norm, multigrid.cpp:104 after gs.cpp:24, in one pass:
+// the same grid as MODE 0, so the partial sums and the norm are bitwise those
+// of the two separate passes).  Block = 256 lanes = 512 cols,
 // grid (strips, row groups); rows [1+g*R, min(n, 1+(g+1)*R)).
 template <int MODE>
 __global__ __launch_bounds__(256) void k_res_march(const double *__restrict__ u,
@@ -1687,7 +1691,7 @@ __global__ __launch_bounds__(256) void k_res_march(const double *__restrict__ u,
         double2 r2 = z2, x2 = z2, y2 = z2;
         if (act) {
             us = ld2(u + o + pitch + c0);
-            if (MODE != 2) r2 = ld2(rhs + o + c0);
+            if (MODE < 2) r2 = ld2(rhs + o + c0);
             x2 = ld2(v1 + o + c0);
             y2 = ld2(v2 + o + c0);
         }
@@ -1699,14 +1703,26 @@ __global__ __launch_bounds__(256) void k_res_march(const double *__restrict__ u,
         if (act) {
             double2 res = z2;
             bool ok0 = c0 >= 1 && c0 <= n - 1, ok1 = c0 + 1 <= n - 1;
-            if (MODE == 2) {
+            if (MODE == 3) {
+                // rhs (gs.cpp:44) stored, then the residual against it (:75)
+                const double2 f = make_double2(rhs_point(x2.x, y2.x, um.x, un.x, w, us.x, um.y, c),
+                                               rhs_point(x2.y, y2.y, um.y, un.y, um.x, us.y, e, c));
+                if (ok0 && ok1) {
+                    st2(out + o + c0, f);
+                } else {
+                    if (ok0) out[o + c0] = f.x;
+                    if (ok1) out[o + c0 + 1] = f.y;
+                }
+                res.x = res_point(f.x, x2.x, y2.x, um.x, un.x, w, us.x, um.y, c);
+                res.y = res_point(f.y, x2.y, y2.y, um.y, un.y, um.x, us.y, e, c);
+            } else if (MODE == 2) {
                 res.x = rhs_point(x2.x, y2.x, um.x, un.x, w, us.x, um.y, c);
                 res.y = rhs_point(x2.y, y2.y, um.y, un.y, um.x, us.y, e, c);
             } else {
                 res.x = res_point(r2.x, x2.x, y2.x, um.x, un.x, w, us.x, um.y, c);
                 res.y = res_point(r2.y, x2.y, y2.y, um.y, un.y, um.x, us.y, e, c);
             }
-            if (MODE == 0) {
+            if (MODE == 0 || MODE == 3) {
                 if (ok0) acc += res.x * res.x;
                 if (ok1) acc += res.y * res.y;
             } else {
@@ -1721,7 +1737,7 @@ __global__ __launch_bounds__(256) void k_res_march(const double *__restrict__ u,
         un = um;
         um = us;
     }
-    if (MODE == 0) {
+    if (MODE == 0 || MODE == 3) {
         double tot = block_sum(acc, lds);
         if (t == 0) partials[blockIdx.y * gridDim.x + blockIdx.x] = tot;
     }
@@ -2453,6 +2469,20 @@ void launch_rhs(double *rhs, const double *u, const double *v1, const double *v2
     res_grid(n, e - f, g, R);
     MGX_LAUNCH((k_res_march<2>), g, dim3(256), s, u, (const double *)nullptr, v1, v2, (int)n,
                pitch, c, R, rhs, (double *)nullptr, f, e);
+}
+
+void launch_rhs_norm(double *rhs, const double *u, const double *v1, const double *v2, long n,
+                     long pitch, Coef c, double *partials, double *out, hipStream_t s, int ra,
+                     int rb, bool take_sqrt) {
+    int f, e;
+    interior_rows(n, ra, rb, f, e);
+    dim3 g;
+    int R;
+    res_grid(n, e - f, g, R);
+    MGX_LAUNCH((k_res_march<3>), g, dim3(256), s, u, (const double *)nullptr, v1, v2, (int)n,
+               pitch, c, R, rhs, partials, f, e);
+    MGX_LAUNCH(k_norm_final, dim3(1), dim3(kFinalThreads), s, (const double *)partials,
+               (int)(g.x * g.y), out, take_sqrt ? 1 : 0);
 }
 
 void launch_residual_restrict(const double *u, const double *rhs, const double *v1,

@@ -360,6 +360,19 @@ int op_rhs(mgx_ctx *c) {
     });
 }
 
+// compute_rhs (gs.cpp:24) + mg_outer's initial residual norm (multigrid.cpp:104)
+// in one pass over u, v1, v2 (a time step's first two reads of the fields)
+static int op_rhs_norm(mgx_ctx *c, double *res0) {
+    drop_spec(c);
+    CHK(materialize(c, 0));
+    Level &L = c->lv[0];
+    CHK(launch(c, MGX_K_RHS, 0, 32.0 * L.M() + 48.0 * L.M(), 32.0 * L.M(), [&] {
+        mgx::launch_rhs_norm(L.rhs, L.U(), L.v1, L.v2, L.n, L.pitch, L.coef, c->partials,
+                             c->dscal, c->stream);
+    }));
+    return read_norm(c, res0);
+}
+
 // mg_outer (multigrid.cpp:97-120).
 // one V-cycle + the residual norm after it, single GPU or partitioned
 // store_post = false: the caller runs another cycle right away, so this
@@ -373,9 +386,14 @@ int norm0(mgx_ctx *c, double *res) {
     return op_residual_norm(c, 0, res);
 }
 
-int op_mg_outer(mgx_ctx *c, double tol, int *cycles, double *res0_out, double *res_out) {
+// have_res0: the caller computed the initial norm (fused with compute_rhs)
+int op_mg_outer(mgx_ctx *c, double tol, int *cycles, double *res0_out, double *res_out,
+                const double *have_res0 = nullptr) {
     double res0 = 0, res = 0;
-    CHK(norm0(c, &res0));
+    if (have_res0)
+        res0 = *have_res0;
+    else
+        CHK(norm0(c, &res0));
     res = res0;
     int iter = 0;
     for (; iter < c->opt.max_cycle && res / res0 > tol; ++iter) CHK(cycle_norm(c, &res));
@@ -733,8 +751,11 @@ int mgx_mg_outer(mgx_ctx *c, double tol, int *cycles, double *res0, double *res)
 }
 int mgx_step(mgx_ctx *c, double tol, int *cycles) {
     if (!c) return fail(MGX_E_ARG, "null ctx");
-    CHK(c->dist ? dist_rhs(c) : op_rhs(c));
-    return op_mg_outer(c, tol, cycles, nullptr, nullptr);
+    // compute_rhs and mg_outer's initial norm in one pass (timestepper,
+    // multigrid.cpp:168-170)
+    double res0 = 0;
+    CHK(c->dist ? dist_rhs_norm(c, &res0) : op_rhs_norm(c, &res0));
+    return op_mg_outer(c, tol, cycles, nullptr, nullptr, &res0);
 }
 int mgx_run_cycles(mgx_ctx *c, int cycles, double *res) {
     if (!c || cycles < 0) return fail(MGX_E_ARG, "mgx_run_cycles: bad args");

@@ -216,3 +216,29 @@ def test_config2_bitwise_vs_nu2_reference(golden_summary):
         cyc = [mg.step(1e-6) for _ in range(st["steps"])]
         assert cyc == st["cycles"]
         assert hashlib.sha256(mg.download().tobytes()).hexdigest() == st["sha256"]
+
+
+@pytest.mark.parametrize("G", [1, 4], ids=["single", "G4"])
+def test_step_fused_rhs_norm_equals_rhs_then_mg_outer(G):
+    """mgx_step computes compute_rhs and mg_outer's initial residual norm in
+    one pass (k_res_march<3>); rhs() + mg_outer() runs them as two.  Same
+    cycle counts and bitwise the same u over three time steps, on one GPU and
+    on row blocks."""
+    N, L = 1024, 6
+    dt, tol = 1.0 / N / 10, 1e-6
+    u0, v1, v2 = init_problem(N)
+    kw = dict(local_parts=G) if G > 1 else {}
+    out = []
+    for fused in (False, True):
+        with Multigrid(N, L, dt, NU, **kw) as mg:
+            mg.upload(u0, v1, v2)
+            cyc = []
+            for _ in range(3):
+                if fused:
+                    cyc.append(mg.step(tol))
+                else:
+                    mg.rhs()
+                    cyc.append(mg.mg_outer(tol)[0])
+            out.append((cyc, mg.download()))
+    assert out[0][0] == out[1][0]
+    assert np.array_equal(out[0][1], out[1][1])
