@@ -63,6 +63,11 @@ void launch_gs_sweep(const double *uin, double *uout, const double *rhs, const d
 // of workgroups launched, -1 for an unsupported (sweeps, mode).
 constexpr int kSmoothMaxSweeps = 3;
 enum : int { kModeZero = 1, kModeProlong = 2, kModeRestrict = 4, kModeNorm = 8 };
+// Mode bit 16 (with kModeRestrict, row march only, sweeps 2-3): the rhs is
+// computed from uin on the fly (compute_rhs, gs.cpp:44) and stored to rhs_out,
+// and the residual norm of uin against it goes to *norm_out -- a time step's
+// compute_rhs, mg_outer's initial norm and the first pre-smoothing in one pass.
+constexpr int kModeRhsNorm = 16;
 struct SmoothArgs {
     const double *uin;
     double *uout;
@@ -74,6 +79,7 @@ struct SmoothArgs {
     long pitchc;        // pitch of the coarse level
     double *partials;   // NORM
     double *norm_out;   // NORM: sqrt of the sum (norm_sqrt) or the plain sum
+    double *rhs_out = nullptr;   // kModeRhsNorm: the computed rhs
     bool norm_sqrt = true;
     bool norm_accumulate = false;   // NORM: add the plain sum to *norm_out
     // Row-block partitions (multi-GPU): output rows [ra, rb) and rows [lo, hi]

@@ -597,6 +597,11 @@ struct WCfg {
     static constexpr bool PROL = (MODE & 2) != 0;
     static constexpr bool REST = (MODE & 4) != 0;
     static constexpr bool NORM = (MODE & 8) != 0;
+    // RHSN: the rhs is computed on the fly from the (original) u rows as they
+    // enter the ring (gs.cpp:44), stored, and the residual of u against it
+    // summed (mg_outer's initial norm, multigrid.cpp:104) -- a time step's
+    // compute_rhs, initial norm and first pre-smoothing in one pass
+    static constexpr bool RHSN = (MODE & 16) != 0;
     static constexpr int S = 2 * K;
     static constexpr int E = S + ((REST || NORM) ? 1 : 0);
     static constexpr int H = (E + 1) / 2;
@@ -640,6 +645,13 @@ __device__ __forceinline__ double res_point_t(double rhs, double t1, double t2, 
     const double cc = c.rr * (c.nu - t1), dd = c.rr * (t1 + c.nu);
     return rhs - (c.dgs * u + cc * uN + aa * uW + dd * uS + bb * uE);
 }
+// gs.cpp:44 with t1, t2
+__device__ __forceinline__ double rhs_point_t(double t1, double t2, double u, double uN,
+                                              double uW, double uS, double uE, const Coef &c) {
+    const double aa = c.rr * (c.nu - t2), bb = c.rr * (t2 + c.nu);
+    const double cc = c.rr * (c.nu - t1), dd = c.rr * (t1 + c.nu);
+    return c.drhs * u - cc * uN - aa * uW - dd * uS - bb * uE;
+}
 
 // G = false: the unguarded march (interior strips, rows [TOP, n+1-BOT) of
 // WCfg: no per-stage predicates), G = true: guarded (see k_xsmooth).
@@ -648,12 +660,13 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
     const double *__restrict__ uin, double *__restrict__ uout, const double *__restrict__ rhs,
     const double *__restrict__ v1, const double *__restrict__ v2, const double *__restrict__ uc,
     long pitchc, double *__restrict__ rhsc, double *__restrict__ partials, int n, long pitch,
-    MarchRegions reg, long units_per_wg, Coef c, int lo, int hi) {
+    MarchRegions reg, long units_per_wg, Coef c, int lo, int hi, double *__restrict__ rhs_out) {
     using C = WCfg<K, MODE>;
     constexpr int S = C::S, E = C::E, H = C::H, NR = C::NR, W = C::W;
     // rhs/v prefetch distance in steps (row s+WRV takes the slot of row
-    // s+WRV-NR, last used by the residual stage on row s+1-S)
-    constexpr int WRV = MGX_WRV;
+    // s+WRV-NR, last used by the residual stage on row s+1-S); RHSN uses a
+    // row's v two steps before its first stage
+    constexpr int WRV = C::RHSN ? (MGX_WRV > 4 ? MGX_WRV : 4) : MGX_WRV;
     static_assert(WRV >= 2 && WRV <= NR - S + 1, "rhs/v prefetch distance");
     // WPB waves per workgroup march WPB adjacent strips over the same rows,
     // independently (no barriers); their row loads are adjacent 1-KiB pieces
@@ -729,7 +742,7 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
         // rhs and t = v*h/2 of row R
         auto load_rv = [&](int R, RowData &d) {
             const long o = (long)min(max(R, lo), hi) * pitch;
-            d.r = ld2((rhs + o) + cl);
+            if (!C::RHSN) d.r = ld2((rhs + o) + cl);
             const double2 x = ld2((v1 + o) + cl), y = ld2((v2 + o) + cl);
             d.x = make_double2(x.x * hh, x.y * hh);
             d.y = make_double2(y.x * hh, y.y * hh);
@@ -758,6 +771,38 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
         load_u(s + 4, up[0]);
 #pragma unroll
         for (int d = 1; d < WRV; ++d) load_rv(s + d, rd[d]);
+        // RHSN: rhs of row r (ring slot iR) from its original u rows r-1..r+1,
+        // stored on the owned interior points, and the residual of u against
+        // it summed (gs.cpp:44, :75; interior, owned rows / lanes only)
+        auto rhs_norm = [&](const int r, const int iR, const int iN, const int iS) {
+            RowData &d = rd[iR];
+            const double uW = dpp_shr1(ur[iR].y), uE = dpp_shl1(ur[iR].x);
+            const double f0 = rhs_point_t(d.x.x, d.y.x, ur[iR].x, ur[iN].x, uW, ur[iS].x,
+                                          ur[iR].y, c);
+            const double f1 = rhs_point_t(d.x.y, d.y.y, ur[iR].y, ur[iN].y, ur[iR].x, ur[iS].y,
+                                          uE, c);
+            d.r = make_double2(f0, f1);
+            if (r >= a && r < b && r >= 1 && r <= n - 1 && keep) {
+                double *row = rhs_out + (long)r * pitch;
+                if (in0 && in1) {
+                    st2(row + c0, d.r);
+                } else {
+                    if (in0) row[c0] = f0;
+                    if (in1) row[c0 + 1] = f1;
+                }
+                if (in0) {
+                    const double res = res_point_t(f0, d.x.x, d.y.x, ur[iR].x, ur[iN].x, uW,
+                                                   ur[iS].x, ur[iR].y, c);
+                    acc += res * res;
+                }
+                if (in1) {
+                    const double res = res_point_t(f1, d.x.y, d.y.y, ur[iR].y, ur[iN].y,
+                                                   ur[iR].x, ur[iS].y, uE, c);
+                    acc += res * res;
+                }
+            }
+        };
+        if (C::RHSN) rhs_norm(s + 1, 1, 0, 2);   // the first stage's row
 
         for (;;) {
 #pragma unroll
@@ -765,6 +810,8 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                 // (1) u row s+3 enters the ring; its prefetch set takes row s+5
                 ur[(p + 3) % NR] = make_u(s + 3, up[(p + 1) & 1], (p + 3) & 1);
                 load_u(s + 5, up[(p + 1) & 1]);
+                // rows s+1..s+3 are still original u: rhs of row s+2
+                if (C::RHSN) rhs_norm(s + 2, (p + 2) % NR, (p + 1) % NR, (p + 3) % NR);
                 // (2) the S smoothing stages
 #pragma unroll
                 for (int h = 0; h < S; ++h) {
@@ -848,7 +895,7 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
         }
     done:;
     }
-    if (C::NORM) {
+    if (C::NORM || C::RHSN) {
         const double tot = wave_sum(acc);
         if (l == 0) partials[(long)blockIdx.x * WPB + wv] = tot;
     }
@@ -2125,7 +2172,7 @@ static int wsmooth_launch(const SmoothArgs &A, const MarchRegions &reg, double *
     const unsigned grid = (unsigned)((total + upw - 1) / upw);
     MGX_LAUNCH((k_wsmooth<WPB, K, MODE, G>), dim3(grid), dim3(64 * WPB), s, A.uin, A.uout,
                A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch,
-               order_regions(reg, upw), upw, A.c, A.lo, A.hi);
+               order_regions(reg, upw), upw, A.c, A.lo, A.hi, A.rhs_out);
     return (int)grid * WPB;   // NORM partials written
 }
 
@@ -2349,8 +2396,8 @@ static int smooth_block(const SmoothArgs &A, hipStream_t s) {
     // the row march needs >= ~32 rows per wave to amortise its priming rows;
     // a row block too small to give every resident wave that much (a
     // partitioned level on many GPUs) runs as LDS tiles instead
-    bool tile = A.n <= tile_max_n();
-    if (!tile) {
+    bool tile = A.n <= tile_max_n() && !(MODE & 16);   // RHSN: march only
+    if (!tile && !(MODE & 16)) {
         constexpr int W4 = WCfg<K, MODE>::W * 4;
         static int slots = 0;
         if (!slots) {
@@ -2384,6 +2431,7 @@ static int smooth_k(const SmoothArgs &A, int mode, hipStream_t s) {
         case 8: return smooth_block<K, 8>(A, s);
         case 9: return smooth_block<K, 9>(A, s);
         case 10: return smooth_block<K, 10>(A, s);
+        case 20: return smooth_block<K, 20>(A, s);
         default: return -1;
     }
 }
@@ -2404,7 +2452,7 @@ int launch_smooth(const SmoothArgs &A0, int sweeps, int mode, hipStream_t s) {
         case 3: blocks = smooth_k<3>(A, mode, s); break;
         default: return -1;
     }
-    if (blocks > 0 && (mode & 8))
+    if (blocks > 0 && (mode & (8 | 16)))
         MGX_LAUNCH(k_norm_final, dim3(1), dim3(kFinalThreads), s, (const double *)A.partials,
                    blocks, A.norm_out, A.norm_accumulate ? 2 : A.norm_sqrt ? 1 : 0);
     return blocks;

@@ -249,6 +249,8 @@ int op_coarse(mgx_ctx *c, int l) {
     return MGX_OK;
 }
 
+long g_step_fuse = 1;   // tuning key "step_fuse"
+
 // Can level 0 run the cross-cycle pass (post of cycle k + pre of cycle k+1)?
 static bool cross_ok(mgx_ctx *c) {
     const Level &L = c->lv[0];
@@ -370,6 +372,53 @@ static int op_rhs_norm(mgx_ctx *c, double *res0) {
         mgx::launch_rhs_norm(L.rhs, L.U(), L.v1, L.v2, L.n, L.pitch, L.coef, c->partials,
                              c->dscal, c->stream);
     }));
+    return read_norm(c, res0);
+}
+
+// A time step's compute_rhs, mg_outer's initial norm AND the first cycle's
+// pre-smoothing + restriction in ONE pass over u, v1, v2 (k_wsmooth mode
+// kModeRhsNorm): u_pre goes to the free buffer and is left as the
+// speculative state the first cycle starts from (Level::spec, as after a
+// cross pass).  Only where the cross-cycle schedule runs (so the first cycle
+// takes that state) and level 0 is a row march.  -> false: not applicable.
+static bool step_fusable(mgx_ctx *c) {
+    return cross_ok(c) && c->lv[0].n > mgx::get_tile_max_n() && g_step_fuse != 0;
+}
+static int op_rhs_norm_pre(mgx_ctx *c, double *res0) {
+    drop_spec(c);
+    CHK(materialize(c, 0));
+    CHK(materialize(c, 1));
+    Level &L = c->lv[0], &Cl = c->lv[1];
+    const int k = c->opt.nsmooth;
+    const int out = L.nxt();
+    mgx::SmoothArgs A{};
+    A.uin = L.u[L.cur];
+    A.uout = L.u[out];
+    A.rhs = L.rhs;
+    A.rhs_out = L.rhs;
+    A.v1 = L.v1;
+    A.v2 = L.v2;
+    A.n = L.n;
+    A.pitch = L.pitch;
+    A.c = L.coef;
+    A.uc = Cl.U();
+    A.rhsc = Cl.rhs;
+    A.pitchc = Cl.pitch;
+    A.partials = c->partials;
+    A.norm_out = c->dscal;
+    // algorithmic: compute_rhs 32, residual+norm 48, k sweeps 40 each,
+    // residual+restriction 40 + 24 per coarse point; compulsory: u, v1, v2
+    // read, rhs and u_pre written, the coarse rhs written
+    const double bytes = (32.0 + 48.0 + 40.0 * k + 40.0) * L.M() + 24.0 * Cl.M();
+    const double cbytes = 8.0 * (5.0 * L.M() + Cl.M());
+    int blocks = 0;
+    CHK(launch(c, MGX_K_RHS, 0, bytes, cbytes, [&] {
+        blocks = mgx::launch_smooth(A, k, mgx::kModeRestrict | mgx::kModeRhsNorm, c->stream);
+    }));
+    if (blocks < 0) return fail(MGX_E_ARG, "launch_smooth: rhs+norm+pre-smoothing unsupported");
+    L.spec = out;   // the first cycle's pre-smoothed u (op_vcycle takes it)
+    L.zero = false;
+    Cl.zero = true;
     return read_norm(c, res0);
 }
 
@@ -752,9 +801,14 @@ int mgx_mg_outer(mgx_ctx *c, double tol, int *cycles, double *res0, double *res)
 int mgx_step(mgx_ctx *c, double tol, int *cycles) {
     if (!c) return fail(MGX_E_ARG, "null ctx");
     // compute_rhs and mg_outer's initial norm in one pass (timestepper,
-    // multigrid.cpp:168-170)
+    // multigrid.cpp:168-170), with the first pre-smoothing where it fuses
     double res0 = 0;
-    CHK(c->dist ? dist_rhs_norm(c, &res0) : op_rhs_norm(c, &res0));
+    if (c->dist)
+        CHK(dist_rhs_norm(c, &res0));
+    else if (step_fusable(c))
+        CHK(op_rhs_norm_pre(c, &res0));
+    else
+        CHK(op_rhs_norm(c, &res0));
     return op_mg_outer(c, tol, cycles, nullptr, nullptr, &res0);
 }
 int mgx_run_cycles(mgx_ctx *c, int cycles, double *res) {
@@ -994,6 +1048,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgx::set_xtile_max_rows(value);
         return MGX_OK;
     }
+    if (!strcmp(key, "step_fuse")) {
+        if (value != 0 && value != 1) return fail(MGX_E_ARG, "step_fuse must be 0 or 1");
+        mgxi::g_step_fuse = value;
+        return MGX_OK;
+    }
     if (!strcmp(key, "coarse_lds")) {
         if (value != 0 && value != 1) return fail(MGX_E_ARG, "coarse_lds must be 0 or 1");
         mgx::set_coarse_lds(value);
@@ -1042,6 +1101,10 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "xtile_max_rows")) {
         *value = mgx::get_xtile_max_rows();
+        return MGX_OK;
+    }
+    if (!strcmp(key, "step_fuse")) {
+        *value = mgxi::g_step_fuse;
         return MGX_OK;
     }
     if (!strcmp(key, "coarse_lds")) {

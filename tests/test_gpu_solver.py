@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 from conftest import load_golden
 
-from hpcclassmultigridproject_amd import Multigrid, init_problem, timestepper
+from hpcclassmultigridproject_amd import Multigrid, _lib, init_problem, timestepper
 
 pytestmark = pytest.mark.gpu
 NU = -4e-4
@@ -218,27 +218,36 @@ def test_config2_bitwise_vs_nu2_reference(golden_summary):
         assert hashlib.sha256(mg.download().tobytes()).hexdigest() == st["sha256"]
 
 
-@pytest.mark.parametrize("G", [1, 4], ids=["single", "G4"])
-def test_step_fused_rhs_norm_equals_rhs_then_mg_outer(G):
+@pytest.mark.parametrize("N,G,fuse", [(1024, 1, 1), (1024, 4, 1), (4096, 1, 1), (4096, 1, 0),
+                                      (8192, 1, 1)],
+                         ids=["N1024", "N1024_G4", "N4096", "N4096_nofuse", "N8192"])
+def test_step_fused_rhs_norm_equals_rhs_then_mg_outer(N, G, fuse):
     """mgx_step computes compute_rhs and mg_outer's initial residual norm in
-    one pass (k_res_march<3>); rhs() + mg_outer() runs them as two.  Same
-    cycle counts and bitwise the same u over three time steps, on one GPU and
-    on row blocks."""
-    N, L = 1024, 6
+    one pass (k_res_march<3>), and on a row-march finest level (n >= 4096)
+    the first cycle's pre-smoothing in the same pass too (k_wsmooth mode
+    kModeRhsNorm, tuning key step_fuse); rhs() + mg_outer() runs them as
+    separate passes.  Same cycle counts and bitwise the same u over three
+    time steps, on one GPU and on row blocks."""
+    L = 6
     dt, tol = 1.0 / N / 10, 1e-6
     u0, v1, v2 = init_problem(N)
     kw = dict(local_parts=G) if G > 1 else {}
     out = []
-    for fused in (False, True):
-        with Multigrid(N, L, dt, NU, **kw) as mg:
-            mg.upload(u0, v1, v2)
-            cyc = []
-            for _ in range(3):
-                if fused:
-                    cyc.append(mg.step(tol))
-                else:
-                    mg.rhs()
-                    cyc.append(mg.mg_outer(tol)[0])
-            out.append((cyc, mg.download()))
+    old = _lib.get_tuning("step_fuse")
+    _lib.set_tuning("step_fuse", fuse)
+    try:
+        for fused in (False, True):
+            with Multigrid(N, L, dt, NU, **kw) as mg:
+                mg.upload(u0, v1, v2)
+                cyc = []
+                for _ in range(3):
+                    if fused:
+                        cyc.append(mg.step(tol))
+                    else:
+                        mg.rhs()
+                        cyc.append(mg.mg_outer(tol)[0])
+                out.append((cyc, mg.download()))
+    finally:
+        _lib.set_tuning("step_fuse", old)
     assert out[0][0] == out[1][0]
     assert np.array_equal(out[0][1], out[1][1])
