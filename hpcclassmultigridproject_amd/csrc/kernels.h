@@ -141,6 +141,10 @@ long get_march_order();
 // longer segments amortise the warm-up rows, more keep more waves in flight.
 void set_march_min_rows(long v);
 long get_march_min_rows();
+// 1 (default): a march whose last band would be short runs one full-height
+// segment per workgroup instead (partitioned levels); 0 = equal units only.
+void set_march_seg(long v);
+long get_march_seg();
 // One colour, in place (two launches make a sweep).  Reference for A/B timing.
 void launch_gs_colour(double *u, const double *rhs, const double *v1, const double *v2,
                       long n, long pitch, Coef c, int colour, hipStream_t s);

@@ -524,13 +524,18 @@ struct SmoothCfg {
 // so that with band[k] = units per workgroup, workgroup (band b, group j)
 // marches rows [r0 + b*band, +band) of group j and the workgroups of
 // neighbouring groups march the same rows at the same time.  xcd = 1: the
-// workgroup order is dealt XCD-contiguous (wg_order).
+// workgroup order is dealt XCD-contiguous (wg_order).  seg = 1 (one region,
+// band[0] > 0): workgroup (band b, group j) marches exactly that segment,
+// also in a shorter last band (march_units): with units_per_wg = band the
+// workgroups of a partial last band would each march pieces of several
+// groups, each paying a warm-up.
 struct MarchRegions {
     int sfirst[4], slim[4], r0[4], r1[4];
     int band[4];
     long pre[5];
     int count;
     int xcd;
+    int seg;
 };
 // -> (strip of wave / pair `w` of the group, a, b) of the segment starting at
 // unit `start` (at most `end`); strip < 0: this wave idles on the segment.
@@ -565,6 +570,23 @@ __device__ __forceinline__ long wg_order(const MarchRegions &reg) {
     if (!reg.xcd) return b;
     const int G = gridDim.x, q = G >> 3, r = G & 7, x = b & 7;
     return (long)x * q + min(x, r) + (b >> 3);
+}
+
+// The units [start, end) a workgroup of a march launch works on.
+__device__ __forceinline__ void march_units(const MarchRegions &reg, int wpb, long upw,
+                                            long &start, long &end) {
+    const long w = wg_order(reg);
+    if (!reg.seg) {
+        start = w * upw;
+        end = min(reg.pre[reg.count], start + upw);
+        return;
+    }
+    const int ng = (reg.slim[0] - reg.sfirst[0] + wpb - 1) / wpb;
+    const int B = reg.band[0], rows = reg.r1[0] - reg.r0[0];
+    const int bb = (int)(w / ng), j = (int)(w % ng);
+    const int h = max(0, min(B, rows - bb * B));
+    start = (long)bb * ng * B + (long)j * h;
+    end = start + h;
 }
 
 // k_wsmooth: the fused K-sweep pass of k_smooth as a WAVE-PRIVATE march.
@@ -673,9 +695,8 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
     // of the same rows, issued at about the same time
     const int l = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
-    const long total = reg.pre[reg.count];
-    long start = wg_order(reg) * units_per_wg;
-    const long end = min(total, start + units_per_wg);
+    long start, end;
+    march_units(reg, WPB, units_per_wg, start, end);
     const int nc = n >> 1;
     const double hh = c.h * 0.5;
     double acc = 0.0;
@@ -986,9 +1007,8 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     const int wv = threadIdx.x >> 6;
     const bool isA = wv < WPB;   // wave-uniform role
     const int pr = isA ? wv : wv - WPB;
-    const long total = reg.pre[reg.count];
-    long start = wg_order(reg) * units_per_wg;
-    const long end = min(total, start + units_per_wg);
+    long start, end;
+    march_units(reg, WPB, units_per_wg, start, end);
     const int nc = n >> 1;
     const double hh = c.h * 0.5;
     double acc = 0.0;
@@ -2152,6 +2172,41 @@ static MarchRegions order_regions(const MarchRegions &reg, long upw) {
     return r;
 }
 
+long g_march_seg = 1;   // tuning key "march_seg"
+void set_march_seg(long v) { g_march_seg = v; }
+long get_march_seg() { return g_march_seg; }
+
+// Work plan of a march launch over `reg`: workgroups, units per workgroup and
+// the ordered regions.  Equal units per workgroup, band-major -- except that
+// when the last band is short (a row block of a partitioned level: 2048 rows
+// in bands of 328) its workgroups would each march pieces of several groups,
+// every piece paying the warm-up of ~`warm` rows; then k full-height bands of
+// one segment per workgroup (seg) when that gives the shorter longest march
+// (level 0 at G=8: 492 -> 382 steps).
+static unsigned plan_march(const MarchRegions &reg, int wpb, long slots, long min_rows,
+                           long max_wgs, int warm, long &upw, MarchRegions &out) {
+    const long total = reg.pre[reg.count];
+    long g = std::max<long>(1, std::min<long>(slots, total / min_rows));
+    g = std::min(g, max_wgs);
+    upw = (total + g - 1) / g;
+    unsigned grid = (unsigned)((total + upw - 1) / upw);
+    out = order_regions(reg, upw);
+    if (!g_march_seg || out.count != 1 || out.band[0] <= 0) return grid;
+    const long rows = out.r1[0] - out.r0[0];
+    const long ng = (out.slim[0] - out.sfirst[0] + wpb - 1) / wpb;
+    const long hl = rows % upw;   // height of the last band
+    if (hl == 0) return grid;
+    const long cur = upw + ((upw + hl - 1) / hl) * warm;   // its longest march
+    const long k = std::min(slots, max_wgs) / ng;          // bands of one segment each
+    if (k < 1) return grid;
+    const long B = (rows + k - 1) / k;
+    if (B + warm >= cur) return grid;
+    out.band[0] = (int)B;
+    out.seg = 1;
+    upw = B;
+    return (unsigned)(ng * ((rows + B - 1) / B));
+}
+
 template <int WPB, int K, int MODE, bool G>
 static int wsmooth_launch(const SmoothArgs &A, const MarchRegions &reg, double *partials,
                           long max_wgs, hipStream_t s) {
@@ -2166,13 +2221,14 @@ static int wsmooth_launch(const SmoothArgs &A, const MarchRegions &reg, double *
                                                            64 * WPB, 0);
         slots = std::max(1, cus) * std::max(1, per);
     }
-    long g = std::max<long>(1, std::min<long>(slots, total / march_min_rows()));
-    g = std::min<long>(g, max_wgs);
-    const long upw = (total + g - 1) / g;
-    const unsigned grid = (unsigned)((total + upw - 1) / upw);
+    long upw;
+    MarchRegions r;
+    // (one segment per workgroup measured +4 % on the wave march's levels 1-2
+    // of row blocks: warm = 0 keeps equal shares there)
+    const unsigned grid = plan_march(reg, WPB, slots, march_min_rows(), max_wgs, 0, upw, r);
     MGX_LAUNCH((k_wsmooth<WPB, K, MODE, G>), dim3(grid), dim3(64 * WPB), s, A.uin, A.uout,
-               A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch,
-               order_regions(reg, upw), upw, A.c, A.lo, A.hi, A.rhs_out);
+               A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch, r, upw,
+               A.c, A.lo, A.hi, A.rhs_out);
     return (int)grid * WPB;   // NORM partials written
 }
 
@@ -2211,13 +2267,14 @@ static int xsmooth_launch(const XArgs &A, const MarchRegions &reg, double *parti
                           long min_rows, long max_wgs, hipStream_t s) {
     const long total = reg.pre[reg.count];
     if (total <= 0) return 0;
-    long g = std::max<long>(1, std::min<long>(xsmooth_slots<WPB, K, G>(), total / min_rows));
-    g = std::min(g, max_wgs);
-    const long upw = (total + g - 1) / g;
-    const unsigned grid = (unsigned)((total + upw - 1) / upw);
+    long upw;
+    MarchRegions r;
+    using X = XCfg<K>;
+    const unsigned grid = plan_march(reg, WPB, xsmooth_slots<WPB, K, G>(), min_rows, max_wgs,
+                                     X::EA + X::EB + X::D + X::NR / 2, upw, r);
     MGX_LAUNCH((k_xsmooth<WPB, K, G>), dim3(grid), dim3(128 * WPB), s, A.uin, A.upost, A.upre,
-               A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch,
-               order_regions(reg, upw), upw, A.c, lo, hi, A.store_post ? 1 : 0);
+               A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch, r, upw,
+               A.c, lo, hi, A.store_post ? 1 : 0);
     return (int)grid * 2 * WPB;
 }
 

@@ -1048,6 +1048,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgx::set_xtile_max_rows(value);
         return MGX_OK;
     }
+    if (!strcmp(key, "march_seg")) {
+        if (value != 0 && value != 1) return fail(MGX_E_ARG, "march_seg must be 0 or 1");
+        mgx::set_march_seg(value);
+        return MGX_OK;
+    }
     if (!strcmp(key, "step_fuse")) {
         if (value != 0 && value != 1) return fail(MGX_E_ARG, "step_fuse must be 0 or 1");
         mgxi::g_step_fuse = value;
@@ -1101,6 +1106,10 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "xtile_max_rows")) {
         *value = mgx::get_xtile_max_rows();
+        return MGX_OK;
+    }
+    if (!strcmp(key, "march_seg")) {
+        *value = mgx::get_march_seg();
         return MGX_OK;
     }
     if (!strcmp(key, "step_fuse")) {

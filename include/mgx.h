@@ -187,6 +187,10 @@ int mgx_synchronize(mgx_ctx *ctx);
  * XCD-contiguous.  "tile32_min_n": K=3 tile passes on levels n >= value use
  * 32-row tiles (default 2048).  "march_min_rows": fewest rows per workgroup
  * of a wave-march launch (default 64, >= 8).
+ * "march_seg": 1 (default) gives each workgroup of a row march one
+ * full-height segment when equal shares would leave a short last band whose
+ * workgroups march pieces of several strips (row blocks of a partitioned
+ * level); 0 = equal shares only.
  * "step_fuse": 1 (default) runs a time step's compute_rhs, mg_outer's initial
  * residual norm and the first cycle's finest pre-smoothing as one pass
  * (single GPU, cross-cycle schedule, row-march finest level); 0 = the rhs and

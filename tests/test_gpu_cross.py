@@ -224,3 +224,19 @@ def test_negative_diagonal_routes_to_general_division(cross, oracle_mod):
     for _ in range(2):
         t.mg_inner(dt, nu)
     assert np.array_equal(out[1], t.ufine)
+
+
+@pytest.mark.parametrize("N,L,G", [(8192, 6, 8), (4096, 6, 4)], ids=["N8192_G8", "N4096_G4"])
+def test_one_segment_per_workgroup_plan(N, L, G, cross, knobs):
+    """march_seg: on row blocks whose last band would be short, the marches
+    give each workgroup one full-height segment instead of equal unit shares;
+    only the work split changes: u bitwise, norms to the summation-order
+    tolerance."""
+    cross(1)
+    kw = dict(local_parts=G)
+    knobs(march_seg=0)
+    u0_, n0 = _cycles_plain(N, L, 3, **kw)
+    knobs(march_seg=1)
+    u1_, n1 = _cycles_plain(N, L, 3, **kw)
+    assert np.array_equal(u0_, u1_)
+    np.testing.assert_allclose(n1, n0, rtol=NORM_RTOL)
