@@ -36,6 +36,7 @@ struct Level {
     // pre-smoothed u (written by the cross-cycle pass, with rhs[1] restricted
     // from it and u[1] flagged zero), or -1
     int spec = -1;
+    int xin = -1;   // finest level: the input buffer of the last cross-cycle pass
     int nxt() const { return cur == 0 ? 1 : 0; }   // ping-pong partner of cur
     double *rhs = nullptr, *v1 = nullptr, *v2 = nullptr;
     mgx::Coef coef{};

@@ -303,6 +303,7 @@ static int op_cross(mgx_ctx *c, bool store_post) {
     CHK(launch(c, MGX_K_XSMOOTH, 0, bytes, cbytes,
                [&] { blocks = mgx::launch_xsmooth(A, k, c->stream); }));
     if (blocks < 0) return fail(MGX_E_ARG, "launch_xsmooth: unsupported sweeps");
+    L.xin = L.cur;
     L.cur = P;
     L.spec = Q;
     L.zero = false;
@@ -436,6 +437,27 @@ int norm0(mgx_ctx *c, double *res) {
 }
 
 // have_res0: the caller computed the initial norm (fused with compute_rhs)
+// The cycle that converged did not store its u_post (predicted to go on):
+// recompute it from the cycle's input and the level-1 correction, both still
+// intact -- the post-smoothing pass alone, bitwise the cross pass's u_post
+// (the same prolongation and sweeps: tests/test_gpu_cross.py).
+static int op_redo_post(mgx_ctx *c) {
+    Level &L = c->lv[0];
+    if (L.xin < 0) return fail(MGX_E_INTERNAL, "redo post-smoothing: no cross pass input");
+    L.cur = L.xin;
+    L.spec = -1;
+    L.zero = false;
+    c->lv[1].zero = false;   // u[1] still holds the correction the pass prolonged
+    return op_smooth(c, 0, c->opt.nsmooth, /*prolong=*/true, false, false, nullptr);
+}
+
+// tuning key "post_predict": mg_outer stores a cycle's u_post only when the
+// cycle is predicted to converge -- its norm extrapolated with the last
+// reduction factor within post_predict x tol -- and recomputes it in the
+// rare case a cycle converges unannounced (0 = always store; -1 = never
+// store, always recompute: the test of the recompute path)
+double g_post_predict = 10.0;
+
 int op_mg_outer(mgx_ctx *c, double tol, int *cycles, double *res0_out, double *res_out,
                 const double *have_res0 = nullptr) {
     double res0 = 0, res = 0;
@@ -445,7 +467,20 @@ int op_mg_outer(mgx_ctx *c, double tol, int *cycles, double *res0_out, double *r
         CHK(norm0(c, &res0));
     res = res0;
     int iter = 0;
-    for (; iter < c->opt.max_cycle && res / res0 > tol; ++iter) CHK(cycle_norm(c, &res));
+    // the u_post of a cycle that does not converge is never observed: the
+    // cross pass skips storing it (2.15 GB at N=16384) when so predicted
+    const bool predict = g_post_predict != 0 && !c->dist && cross_ok(c);
+    double prev = res0;
+    for (; iter < c->opt.max_cycle && res / res0 > tol; ++iter) {
+        bool store = true;
+        if (predict && iter + 1 < c->opt.max_cycle) {   // the last allowed cycle always stores
+            const double pred = res * (res / prev);
+            store = g_post_predict > 0 && pred <= g_post_predict * tol * res0;
+        }
+        prev = res;
+        CHK(cycle_norm(c, &res, store));
+        if (!store && !(res / res0 > tol)) CHK(op_redo_post(c));
+    }
     if (cycles) *cycles = iter;
     if (res0_out) *res0_out = res0;
     if (res_out) *res_out = res;
@@ -1048,6 +1083,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgx::set_xtile_max_rows(value);
         return MGX_OK;
     }
+    if (!strcmp(key, "post_predict")) {
+        if (value < -1) return fail(MGX_E_ARG, "post_predict must be >= -1");
+        mgxi::g_post_predict = (double)value;
+        return MGX_OK;
+    }
     if (!strcmp(key, "march_seg")) {
         if (value != 0 && value != 1) return fail(MGX_E_ARG, "march_seg must be 0 or 1");
         mgx::set_march_seg(value);
@@ -1106,6 +1146,10 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "xtile_max_rows")) {
         *value = mgx::get_xtile_max_rows();
+        return MGX_OK;
+    }
+    if (!strcmp(key, "post_predict")) {
+        *value = (long)mgxi::g_post_predict;
         return MGX_OK;
     }
     if (!strcmp(key, "march_seg")) {

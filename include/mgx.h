@@ -195,6 +195,12 @@ int mgx_synchronize(mgx_ctx *ctx);
  * residual norm and the first cycle's finest pre-smoothing as one pass
  * (single GPU, cross-cycle schedule, row-march finest level); 0 = the rhs and
  * norm pass, then the pre-smoothing (bitwise the same results).
+ * "post_predict": mg_outer / step let the cross-cycle pass store a cycle's
+ * post-smoothed u (the value returned if that cycle converges) only when the
+ * cycle's residual, extrapolated with the last cycle's reduction factor, is
+ * within post_predict x tol; a cycle that converges without it is recomputed
+ * by one post-smoothing pass (single GPU; default 10; 0 = always store,
+ * -1 = never store: bitwise the same results).
  * "coarse_lds": 1 (default) solves coarsest levels n <= 64 with the fields
  * in LDS, 0 = through L2 (bitwise the same).
  * None of them changes a result bit. */

@@ -251,3 +251,33 @@ def test_step_fused_rhs_norm_equals_rhs_then_mg_outer(N, G, fuse):
         _lib.set_tuning("step_fuse", old)
     assert out[0][0] == out[1][0]
     assert np.array_equal(out[0][1], out[1][1])
+
+
+@pytest.mark.parametrize("N,maxlvl,nsmooth,tol", [(4096, 5, 3, 1e-6), (4096, 4, 2, 1e-8),
+                                                  (8192, 6, 3, 1e-6)])
+def test_post_predict_recompute_is_bitwise(N, maxlvl, nsmooth, tol):
+    """mg_outer skips storing u_post on cycles predicted not to converge and
+    recomputes it (prolongation + post-smoothing of the cycle's input) when
+    one converges anyway: post_predict -1 (never store, always recompute),
+    10 (the default prediction) and 0 (always store) give the same cycle
+    counts, norms and u, bitwise, over three time steps."""
+    dt = 1.0 / N / 10
+    u0, v1, v2 = init_problem(N)
+    old = _lib.get_tuning("post_predict")
+    out = []
+    try:
+        for pp in (0, -1, 10):
+            _lib.set_tuning("post_predict", pp)
+            with Multigrid(N, maxlvl, dt, NU, nsmooth=nsmooth) as mg:
+                mg.upload(u0, v1, v2)
+                res = []
+                for _ in range(2):
+                    mg.rhs()
+                    res.append(mg.mg_outer(tol)[:3])
+                res.append(mg.step(tol))
+                out.append((res, mg.download()))
+    finally:
+        _lib.set_tuning("post_predict", old)
+    for res, u in out[1:]:
+        assert res == out[0][0]
+        assert np.array_equal(u, out[0][1])
