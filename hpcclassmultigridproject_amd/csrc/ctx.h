@@ -132,6 +132,9 @@ int dist_download(mgx_ctx *c, double *u, hipMemcpyKind kind);
 int dist_rhs(mgx_ctx *c);
 int dist_rhs_norm(mgx_ctx *c, double *res0);
 int dist_vcycle(mgx_ctx *c, double *norm, bool store_post = true);
+// partitioned level 0 runs the cross-cycle pass; recompute its unstored u_post
+bool dist_post_predictable(mgx_ctx *c);
+int dist_redo_post(mgx_ctx *c);
 int dist_residual_norm(mgx_ctx *c, double *norm);
 void dist_free(mgx_ctx *c);
 // replicated coarse-level contexts of a partitioned context (one per local part)

@@ -71,6 +71,7 @@ struct PLevel {
     double *u[3] = {nullptr, nullptr, nullptr};   // u[2]: level 0, cross-cycle pass
     int cur = 0;
     int spec = -1;   // level 0: buffer of the next cycle's pre-smoothed u (Level::spec)
+    int xin = -1;    // level 0: input buffer of the last cross-cycle pass (Level::xin)
     bool zero = false;
     double *rhs = nullptr, *v1 = nullptr, *v2 = nullptr;
     mgx::Coef coef{};
@@ -523,11 +524,37 @@ static int dist_cross(mgx_ctx *c, bool store_post) {
     }
     for (size_t i = 0; i < d->parts.size(); ++i) {
         PLevel &L = d->parts[i].lv[0];
+        L.xin = L.cur;
         L.cur = bufs[i].first;
         L.spec = bufs[i].second;
         L.zero = false;
     }
     return coarse_rhs_ready(c, 0);
+}
+
+bool dist_post_predictable(mgx_ctx *c) {
+    Dist *d = c->dist;
+    return d->la >= 1 && dist_cross_ok(c);
+}
+
+// The last cross pass did not store u_post (mgx.hip:op_redo_post): prolongation
+// + post-smoothing of each row block from the pass's input and the untouched
+// level-1 correction, bitwise the pass's u_post (the unfused schedule).
+int dist_redo_post(mgx_ctx *c) {
+    Dist *d = c->dist;
+    HIPCHK(hipSetDevice(c->device));
+    for (auto &p : d->parts) {
+        PLevel &L = p.lv[0];
+        if (L.xin < 0) return fail(MGX_E_INTERNAL, "redo post-smoothing: no cross pass input");
+        L.cur = L.xin;
+        L.spec = -1;
+        L.zero = false;
+        if (1 < d->la)
+            p.lv[1].zero = false;   // u[1] still holds the correction
+        else
+            p.sub->lv[0].zero = false;
+    }
+    return smooth(c, 0, /*prolong=*/true, false, false);
 }
 
 int dist_vcycle(mgx_ctx *c, double *norm, bool store_post) {

@@ -451,6 +451,21 @@ static int op_redo_post(mgx_ctx *c) {
     return op_smooth(c, 0, c->opt.nsmooth, /*prolong=*/true, false, false, nullptr);
 }
 
+// op_vcycle / dist_vcycle with a norm would run the cross-cycle pass
+static bool post_predictable(mgx_ctx *c) {
+    if (!c->dist) return cross_ok(c);
+    if (dist_la(c) == 0) return cross_ok(dist_sub(c, 0));   // everything replicated
+    return dist_post_predictable(c);
+}
+static int redo_post(mgx_ctx *c) {
+    if (!c->dist) return op_redo_post(c);
+    if (dist_la(c) == 0) {
+        for (int i = 0; i < dist_nsub(c); ++i) CHK(op_redo_post(dist_sub(c, i)));
+        return MGX_OK;
+    }
+    return dist_redo_post(c);
+}
+
 // tuning key "post_predict": mg_outer stores a cycle's u_post only when the
 // cycle is predicted to converge -- its norm extrapolated with the last
 // reduction factor within post_predict x tol -- and recomputes it in the
@@ -469,7 +484,7 @@ int op_mg_outer(mgx_ctx *c, double tol, int *cycles, double *res0_out, double *r
     int iter = 0;
     // the u_post of a cycle that does not converge is never observed: the
     // cross pass skips storing it (2.15 GB at N=16384) when so predicted
-    const bool predict = g_post_predict != 0 && !c->dist && cross_ok(c);
+    const bool predict = g_post_predict != 0 && post_predictable(c);
     double prev = res0;
     for (; iter < c->opt.max_cycle && res / res0 > tol; ++iter) {
         bool store = true;
@@ -479,7 +494,7 @@ int op_mg_outer(mgx_ctx *c, double tol, int *cycles, double *res0_out, double *r
         }
         prev = res;
         CHK(cycle_norm(c, &res, store));
-        if (!store && !(res / res0 > tol)) CHK(op_redo_post(c));
+        if (!store && !(res / res0 > tol)) CHK(redo_post(c));
     }
     if (cycles) *cycles = iter;
     if (res0_out) *res0_out = res0;

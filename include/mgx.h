@@ -199,7 +199,7 @@ int mgx_synchronize(mgx_ctx *ctx);
  * post-smoothed u (the value returned if that cycle converges) only when the
  * cycle's residual, extrapolated with the last cycle's reduction factor, is
  * within post_predict x tol; a cycle that converges without it is recomputed
- * by one post-smoothing pass (single GPU; default 10; 0 = always store,
+ * by one post-smoothing pass (default 10; 0 = always store,
  * -1 = never store: bitwise the same results).
  * "coarse_lds": 1 (default) solves coarsest levels n <= 64 with the fields
  * in LDS, 0 = through L2 (bitwise the same).

@@ -253,22 +253,32 @@ def test_step_fused_rhs_norm_equals_rhs_then_mg_outer(N, G, fuse):
     assert np.array_equal(out[0][1], out[1][1])
 
 
-@pytest.mark.parametrize("N,maxlvl,nsmooth,tol", [(4096, 5, 3, 1e-6), (4096, 4, 2, 1e-8),
-                                                  (8192, 6, 3, 1e-6)])
-def test_post_predict_recompute_is_bitwise(N, maxlvl, nsmooth, tol):
+@pytest.mark.parametrize("N,maxlvl,nsmooth,tol,G,min_rows", [
+    (4096, 5, 3, 1e-6, 1, 0), (4096, 4, 2, 1e-8, 1, 0), (8192, 6, 3, 1e-6, 1, 0),
+    (4096, 5, 3, 1e-6, 4, 0),        # row blocks, levels 0-2 partitioned
+    (4096, 4, 3, 1e-6, 2, 8192)],    # every level replicated (la = 0)
+    ids=["N4096", "N4096nu2", "N8192", "N4096_G4", "N4096_G2_replicated"])
+def test_post_predict_recompute_is_bitwise(N, maxlvl, nsmooth, tol, G, min_rows):
     """mg_outer skips storing u_post on cycles predicted not to converge and
     recomputes it (prolongation + post-smoothing of the cycle's input) when
     one converges anyway: post_predict -1 (never store, always recompute),
     10 (the default prediction) and 0 (always store) give the same cycle
-    counts, norms and u, bitwise, over three time steps."""
+    counts, norms and u, bitwise, over three time steps -- on one GPU and on
+    virtual row blocks."""
     dt = 1.0 / N / 10
     u0, v1, v2 = init_problem(N)
     old = _lib.get_tuning("post_predict")
+    old_rows = _lib.get_tuning("dist_min_rows")
+    kw = dict(local_parts=G) if G > 1 else {}
     out = []
     try:
+        if min_rows:
+            _lib.set_tuning("dist_min_rows", min_rows)
         for pp in (0, -1, 10):
             _lib.set_tuning("post_predict", pp)
-            with Multigrid(N, maxlvl, dt, NU, nsmooth=nsmooth) as mg:
+            with Multigrid(N, maxlvl, dt, NU, nsmooth=nsmooth, **kw) as mg:
+                if G > 1:
+                    assert mg.dist_info()[2] == (0 if min_rows else 3)
                 mg.upload(u0, v1, v2)
                 res = []
                 for _ in range(2):
@@ -278,6 +288,7 @@ def test_post_predict_recompute_is_bitwise(N, maxlvl, nsmooth, tol):
                 out.append((res, mg.download()))
     finally:
         _lib.set_tuning("post_predict", old)
+        _lib.set_tuning("dist_min_rows", old_rows)
     for res, u in out[1:]:
         assert res == out[0][0]
         assert np.array_equal(u, out[0][1])
