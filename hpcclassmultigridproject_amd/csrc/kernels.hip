@@ -602,8 +602,8 @@ __device__ __forceinline__ void march_units(const MarchRegions &reg, int wpb, lo
 // Schedule (as k_smooth): at step s stage h (h = 0..S-1, S = 2K) updates
 // its colour in row s+1-h; the residual stage (RESTRICT / NORM) takes row
 // s+1-S; row s+2-S is final and stored.  u rows s-S .. s+3 are live (S+4 =
-// NR rows), rhs/v rows s+1-S .. s+3 (one spare slot, loaded two steps
-// ahead); NR is even and the step loop is unrolled NR times with its start
+// NR rows), rhs/v rows s+1-S .. s+WRV (loaded WRV steps ahead, MGX_WRV);
+// NR is even and the step loop is unrolled NR times with its start
 // aligned to NR, so every ring index and every row parity is a compile-time
 // constant.
 //
@@ -634,8 +634,11 @@ struct WCfg {
     static constexpr int TOP = E + NR + S + 2, BOT = E + 4;
 };
 
+// rhs/v prefetch distance of the wave march: with t = v*h/2 formed at the
+// row's first use (scale_rv), 4 steps measured -3 % on level 1 against 2
+// (3: -2 %, 5: -2 %; tools/ab_libs.sh)
 #ifndef MGX_WRV
-#define MGX_WRV 2
+#define MGX_WRV 4
 #endif
 
 // 64-bit value of lane l-1 (shr) / l+1 (shl); the edge lane reads 0
@@ -760,13 +763,18 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
             }
             return v;
         };
-        // rhs and t = v*h/2 of row R
+        // rhs and v of row R, raw; t = v*h/2 only at the row's first use
+        // (scale_rv): scaled here, the multiplies would wait for the loads
+        // right after issuing them, and no prefetch distance would help
         auto load_rv = [&](int R, RowData &d) {
             const long o = (long)min(max(R, lo), hi) * pitch;
             if (!C::RHSN) d.r = ld2((rhs + o) + cl);
-            const double2 x = ld2((v1 + o) + cl), y = ld2((v2 + o) + cl);
-            d.x = make_double2(x.x * hh, x.y * hh);
-            d.y = make_double2(y.x * hh, y.y * hh);
+            d.x = ld2((v1 + o) + cl);
+            d.y = ld2((v2 + o) + cl);
+        };
+        auto scale_rv = [&](RowData &d) {
+            d.x = make_double2(d.x.x * hh, d.x.y * hh);
+            d.y = make_double2(d.y.x * hh, d.y.y * hh);
         };
 
         const int s_first = a - E;
@@ -823,7 +831,10 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                 }
             }
         };
-        if (C::RHSN) rhs_norm(s + 1, 1, 0, 2);   // the first stage's row
+        if (C::RHSN) {
+            scale_rv(rd[1]);
+            rhs_norm(s + 1, 1, 0, 2);   // the first stage's row
+        }
 
         for (;;) {
 #pragma unroll
@@ -831,6 +842,8 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                 // (1) u row s+3 enters the ring; its prefetch set takes row s+5
                 ur[(p + 3) % NR] = make_u(s + 3, up[(p + 1) & 1], (p + 3) & 1);
                 load_u(s + 5, up[(p + 1) & 1]);
+                // t of the row first used in this step: s+2 (RHSN), else s+1
+                scale_rv(rd[(p + (C::RHSN ? 2 : 1)) % NR]);
                 // rows s+1..s+3 are still original u: rhs of row s+2
                 if (C::RHSN) rhs_norm(s + 2, (p + 2) % NR, (p + 1) % NR, (p + 3) % NR);
                 // (2) the S smoothing stages

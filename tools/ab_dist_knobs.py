@@ -34,5 +34,5 @@ for rnd in range(a.rounds):
             lv.append(round(tl / a.cycles / G, 4))
         mg.profile(False)
         key = ",".join(f"{k}={v}" for (k, _), v in zip(knobs, combo))
-        print(rnd, key, json.dumps({"ms_per_rank": round(ms / G, 4), "per_level_per_rank": lv[:4]}),
+        print(rnd, key, json.dumps({"ms_per_rank": round(ms / G, 4), "per_level_per_rank": lv}),
               flush=True)
