@@ -806,10 +806,16 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
         auto rhs_norm = [&](const int r, const int iR, const int iN, const int iS) {
             RowData &d = rd[iR];
             const double uW = dpp_shr1(ur[iR].y), uE = dpp_shl1(ur[iR].x);
+            // a fresh scalar nu: keeps the compiler from holding this row's
+            // coefficients live until its smoothing stages (MGX_RHSN_CSE)
+            Coef cg = c;
+#ifndef MGX_RHSN_CSE
+            asm volatile("" : "+s"(cg.nu));
+#endif
             const double f0 = rhs_point_t(d.x.x, d.y.x, ur[iR].x, ur[iN].x, uW, ur[iS].x,
-                                          ur[iR].y, c);
+                                          ur[iR].y, cg);
             const double f1 = rhs_point_t(d.x.y, d.y.y, ur[iR].y, ur[iN].y, ur[iR].x, ur[iS].y,
-                                          uE, c);
+                                          uE, cg);
             d.r = make_double2(f0, f1);
             if (r >= a && r < b && r >= 1 && r <= n - 1 && keep) {
                 double *row = rhs_out + (long)r * pitch;
@@ -1330,6 +1336,12 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
 // by one point per stage, so the output tile is exact (same argument as
 // k_smooth).  Each lane owns fixed column pairs of the tile and keeps their
 // rhs / v1 / v2 in registers for all stages.
+// threads per tile workgroup: 1024 (2 pairs per thread, ~80-105 VGPRs)
+// against 256 (8 pairs, 155-189 VGPRs): levels 3-7 0.289 -> 0.237 ms per
+// cycle (512: 0.248), the stages' per-thread chains being the latency
+#ifndef MGX_TILE_THREADS
+#define MGX_TILE_THREADS 1024
+#endif
 template <int K, int MODE, int TRV = 16>
 struct TileCfg {
     using C = SmoothCfg<K, MODE>;
@@ -1337,12 +1349,12 @@ struct TileCfg {
     static constexpr int EH = (C::E + 1) / 2 * 2;         // halo, even
     static constexpr int RT = TR + 2 * EH, WT = TC + 2 * EH;
     static constexpr int PAIRS = RT * WT / 2;
-    static constexpr int THREADS = 256;
+    static constexpr int THREADS = MGX_TILE_THREADS;
     static constexpr int PPT = (PAIRS + THREADS - 1) / THREADS;   // pairs per thread
 };
 
 template <int K, int MODE, int TRV>
-__global__ __launch_bounds__(256) void k_smooth_tile(
+__global__ __launch_bounds__(MGX_TILE_THREADS) void k_smooth_tile(
     const double *__restrict__ uin, double *__restrict__ uout, const double *__restrict__ rhs,
     const double *__restrict__ v1, const double *__restrict__ v2, const double *__restrict__ uc,
     long pitchc, double *__restrict__ rhsc, double *__restrict__ partials, int n, long pitch,
@@ -1374,7 +1386,7 @@ __global__ __launch_bounds__(256) void k_smooth_tile(
     bool ok[PPT];
 #pragma unroll
     for (int m = 0; m < PPT; ++m) {
-        const int q = t + m * 256;
+        const int q = t + m * T::THREADS;
         ok[m] = false;
         f0[m] = f1[m] = x0[m] = x1[m] = y0[m] = y1[m] = 0.0;
         if (q >= T::PAIRS) continue;
@@ -1419,7 +1431,7 @@ __global__ __launch_bounds__(256) void k_smooth_tile(
     unsigned upd = 0, rpar = 0;   // bits 2m / 2m+1: column 2k / 2k+1 updatable; bit m: row odd
 #pragma unroll
     for (int m = 0; m < PPT; ++m) {
-        const int q = t + m * 256;
+        const int q = t + m * T::THREADS;
         xs[m] = 0;
         if (q >= T::PAIRS || !ok[m]) continue;
         const int r = q / HW, k = q % HW;
@@ -1440,7 +1452,7 @@ __global__ __launch_bounds__(256) void k_smooth_tile(
     for (int h = 0; h < S; ++h) {
 #pragma unroll
         for (int m = 0; m < PPT; ++m) {
-            const int q = t + m * 256;
+            const int q = t + m * T::THREADS;
             if (q >= T::PAIRS) continue;
             const int cs = (int)((rpar >> m) & 1u) ^ (h & 1);   // origin parity is even
             if (!((upd >> (2 * m + cs)) & 1u)) continue;
@@ -1458,7 +1470,7 @@ __global__ __launch_bounds__(256) void k_smooth_tile(
     double acc = 0.0;
 #pragma unroll
     for (int m = 0; m < PPT; ++m) {
-        const int q = t + m * 256;
+        const int q = t + m * T::THREADS;
         if (q >= T::PAIRS || !ok[m]) continue;
         const int r = q / HW, k = q % HW;
         if (r < EH || r >= EH + T::TR || 2 * k < EH || 2 * k >= EH + T::TC) continue;
@@ -1490,7 +1502,7 @@ __global__ __launch_bounds__(256) void k_smooth_tile(
         }
     }
     if (C::NORM) {
-        __shared__ double red_lds[4];
+        __shared__ double red_lds[T::THREADS / 64];
         const double tot = block_sum(acc, red_lds);
         if (t == 0) partials[bid] = tot;
     }
@@ -2446,7 +2458,7 @@ static int smooth_tile_rows(const SmoothArgs &A, hipStream_t s) {
     const int tiles_y = (int)((A.rb - A.ra + T::TR - 1) / T::TR);
     const long grid = (long)tiles_x * tiles_y;
     if ((MODE & 8) && grid > kNormBlocks) return -1;
-    MGX_LAUNCH((k_smooth_tile<K, MODE, TRV>), dim3((unsigned)grid), dim3(256), s, A.uin,
+    MGX_LAUNCH((k_smooth_tile<K, MODE, TRV>), dim3((unsigned)grid), dim3(T::THREADS), s, A.uin,
                A.uout, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, A.partials, (int)n, A.pitch,
                tiles_x, A.c, A.ra, A.rb, A.lo, A.hi, tile_xcd() ? 1 : 0);
     return (int)grid;
