@@ -2165,7 +2165,7 @@ static void march_regions(long n, int W, int H, int ra, int rb, int top, int bot
     }
 }
 
-long g_march_min_rows = 64;   // fewest rows per workgroup of a wave march (tuning key)
+long g_march_min_rows = 32;   // fewest rows per workgroup of a wave march (tuning key)
 static long march_min_rows() { return g_march_min_rows; }
 void set_march_min_rows(long v) { g_march_min_rows = v; }
 long get_march_min_rows() { return g_march_min_rows; }

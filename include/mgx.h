@@ -186,7 +186,7 @@ int mgx_synchronize(mgx_ctx *ctx);
  * (env MGX_MARCH_ORDER).  "tile_xcd": 1 (default) deals the LDS tiles
  * XCD-contiguous.  "tile32_min_n": K=3 tile passes on levels n >= value use
  * 32-row tiles (default 2048).  "march_min_rows": fewest rows per workgroup
- * of a wave-march launch (default 64, >= 8).
+ * of a wave-march launch (default 32, >= 8).
  * "march_seg": 1 (default) gives each workgroup of a row march one
  * full-height segment when equal shares would leave a short last band whose
  * workgroups march pieces of several strips (row blocks of a partitioned
