@@ -100,9 +100,20 @@ __device__ __forceinline__ void st2s(double *p, double2 v) {
 }
 // Conditional stores of the march (exec-masked).  A hardware-dropped raw
 // buffer store (offset past the row) would avoid the exec branch, but measured
-// +20 % on the cross pass (3.25 vs 2.72 ms at N=16384), so these stay plain.
+// +20 % on the cross pass (3.25 vs 2.72 ms at N=16384), so these stay
+// branches.  The u rows they write are next read a whole coarse descent or
+// cycle later, so they are streaming stores (MGX_NTST): -1.7 % per V-cycle
+// (level 0 -0.02 ms, level 1 -0.035 ms); the coarse rhs, read by the very next
+// pass, stays a plain store.
+#ifndef MGX_NTST
+#define MGX_NTST 1
+#endif
 __device__ __forceinline__ void st2_if(double *row, int col, bool on, double2 v) {
+#if MGX_NTST
+    if (on) st2s(row + col, v);
+#else
     if (on) st2(row + col, v);
+#endif
 }
 __device__ __forceinline__ void st1_if(double *row, int col, bool on, double v) {
     if (on) row[col] = v;
@@ -881,8 +892,8 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                 // (3) row s+2-S is final
                 {
                     const int ro = s + 2 - S;
-                    if (ro >= a && ro < b && keep)
-                        st2((uout + (long)ro * pitch) + c0, ur[(p + 2 - S + 2 * NR) % NR]);
+                    st2_if(uout + (long)ro * pitch, c0, ro >= a && ro < b && keep,
+                           ur[(p + 2 - S + 2 * NR) % NR]);
                 }
                 // (4) residual stage on row s+1-S
                 if (C::REST || C::NORM) {
