@@ -737,17 +737,20 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
         const int cl = min(max(c0, 0), (int)pitch - 2);
         const int jl = cl >> 1;
         const int j1 = (jl + 1 <= nc) ? 1 : 0;
-        auto load_u = [&](int R, UPre &u) {
+        // (odd = R's parity, a compile-time constant at every call site: an
+        // even row's prolongation needs only the coarse row below it)
+        auto load_u = [&](int R, UPre &u, const bool odd) {
             if (C::ZERO) return;
             const int Rc = min(max(R, lo), hi);
             u.X = ld2((uin + (long)Rc * pitch) + cl);
             if (C::PROL) {
                 const double *p0 = (uc + (long)(Rc >> 1) * pitchc) + jl;
-                const double *p1 = p0 + ((Rc & 1) ? pitchc : 0);
                 u.q00 = p0[0];
                 u.q01 = p0[j1];
-                u.q10 = p1[0];
-                u.q11 = p1[j1];
+                if (odd) {
+                    u.q10 = p0[pitchc];
+                    u.q11 = p0[pitchc + j1];
+                }
             }
         };
         // u row R (+ prolongation) as it enters the ring
@@ -804,11 +807,11 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
         // flight (sets 1 / 0), rhs/v rows s+1, s+2 loaded
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-            load_u(s + d, up[0]);
+            load_u(s + d, up[0], d & 1);
             ur[d] = make_u(s + d, up[0], d & 1);
         }
-        load_u(s + 3, up[1]);
-        load_u(s + 4, up[0]);
+        load_u(s + 3, up[1], true);
+        load_u(s + 4, up[0], false);
 #pragma unroll
         for (int d = 1; d < WRV; ++d) load_rv(s + d, rd[d]);
         // RHSN: rhs of row r (ring slot iR) from its original u rows r-1..r+1,
@@ -858,7 +861,7 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
             for (int p = 0; p < NR; ++p) {
                 // (1) u row s+3 enters the ring; its prefetch set takes row s+5
                 ur[(p + 3) % NR] = make_u(s + 3, up[(p + 1) & 1], (p + 3) & 1);
-                load_u(s + 5, up[(p + 1) & 1]);
+                load_u(s + 5, up[(p + 1) & 1], (p + 1) & 1);
                 // t of the row first used in this step: s+2 (RHSN), else s+1
                 scale_rv(rd[(p + (C::RHSN ? 2 : 1)) % NR]);
                 // rows s+1..s+3 are still original u: rhs of row s+2
@@ -1064,15 +1067,18 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
         UPre up[NR];
 #pragma unroll
         for (int i = 0; i < NR; ++i) up[i] = UPre{make_double2(0.0, 0.0), 0.0, 0.0, 0.0, 0.0};
-        auto load_u = [&](int R, UPre &u) {   // A: u row R + its coarse parents
+        // A: u row R + its coarse parents (odd = R's parity, compile-time:
+        // an even row needs only the coarse row below it)
+        auto load_u = [&](int R, UPre &u, const bool odd) {
             const int Rc = min(max(R, lo), hi);
             u.X = ld2((uin + (long)Rc * pitch) + cl);
             const double *p0 = (uc + (long)(Rc >> 1) * pitchc) + jl;
-            const double *p1 = p0 + ((Rc & 1) ? pitchc : 0);
             u.q00 = p0[0];
             u.q01 = p0[j1];
-            u.q10 = p1[0];
-            u.q11 = p1[j1];
+            if (odd) {
+                u.q10 = p0[pitchc];
+                u.q11 = p0[pitchc + j1];
+            }
         };
         // + prolongation (gs.cpp:238-265); static parity, select (see k_wsmooth)
         auto make_u = [&](int R, const UPre &u, const bool odd) {
@@ -1196,11 +1202,11 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
         if (isA) {
 #pragma unroll
             for (int d = 0; d < 3; ++d) {
-                load_u(s0 + d, up[d]);
+                load_u(s0 + d, up[d], d & 1);
                 ur[d] = make_u(s0 + d, up[d], d & 1);
             }
 #pragma unroll
-            for (int d = 3; d < 3 + XU; ++d) load_u(s0 + d, up[d]);
+            for (int d = 3; d < 3 + XU; ++d) load_u(s0 + d, up[d], d & 1);
 #pragma unroll
             for (int d = 1; d < XRV; ++d) load_rv(s0 + d, rd[d]);
             for (;;) {
@@ -1208,7 +1214,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                 for (int p = 0; p < NR; ++p) {   // s == p (mod NR)
                     const int s = s0 + it + (p & 1);
                     ur[(p + 3) % NR] = make_u(s + 3, up[(p + 3) % NR], (p + 3) & 1);
-                    load_u(s + 3 + XU, up[(p + 3 + XU) % NR]);   // XU steps ahead
+                    load_u(s + 3 + XU, up[(p + 3 + XU) % NR], (p + 3 + XU) & 1);   // XU ahead
 #pragma unroll
                     for (int h = 0; h < S; ++h) stage(ur, rd, p, h, s + 1 - h);
                     // hand-off: rhs/v row s+1 (first used above), final u row s+2-S
