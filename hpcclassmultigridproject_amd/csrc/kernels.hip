@@ -2265,9 +2265,12 @@ static int wsmooth_launch(const SmoothArgs &A, const MarchRegions &reg, double *
     }
     long upw;
     MarchRegions r;
-    // (one segment per workgroup measured +4 % on the wave march's levels 1-2
-    // of row blocks: warm = 0 keeps equal shares there)
-    const unsigned grid = plan_march(reg, WPB, slots, march_min_rows(), max_wgs, 0, upw, r);
+    // one segment per workgroup when the last band is short (warm-up ~E + NR/2
+    // rows: the prologue aligns the first step to NR): level 1 at N=16384
+    // 1.11 -> 1.075 ms (its 19 last-band workgroups each marched pieces of two
+    // strips); the same per rank on 8 row blocks
+    const unsigned grid = plan_march(reg, WPB, slots, march_min_rows(), max_wgs,
+                                     WCfg<K, MODE>::E + WCfg<K, MODE>::NR / 2, upw, r);
     MGX_LAUNCH((k_wsmooth<WPB, K, MODE, G>), dim3(grid), dim3(64 * WPB), s, A.uin, A.uout,
                A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch, r, upw,
                A.c, A.lo, A.hi, A.rhs_out);
