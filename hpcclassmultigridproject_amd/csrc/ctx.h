@@ -69,6 +69,9 @@ struct mgx_ctx {
     double *hscal = nullptr;      // pinned host mirror
     double *stage[2] = {nullptr, nullptr};   // reference-layout (N+1)^2 staging
     mgxi::Dist *dist = nullptr;   // row-partitioned multi-GPU state (dist.hip)
+    // mg_outer's cycle predicted to be the last: its finest level runs the
+    // post-smoothing alone, not the cross pass (no next-cycle pre-smoothing)
+    bool post_only = false;
     // profiling
     int prof = 0;   // 0 off, 1 every launch, 2 finest-level launches only
     std::vector<mgxi::ProfRec> pending;

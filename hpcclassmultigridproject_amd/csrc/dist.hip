@@ -575,6 +575,11 @@ int dist_vcycle(mgx_ctx *c, double *norm, bool store_post) {
             CHK(coarse_rhs_ready(c, 0));
         }
         CHK(coarse_cycle(c, 1));
+        if (c->post_only) {   // mg_outer's last cycle: post-smoothing + norm only
+            CHK(smooth(c, 0, /*prolong=*/true, false, /*norm=*/true));
+            dist_drop_spec(c);
+            return reduce_norm(c, norm);
+        }
         CHK(dist_cross(c, store_post));
         return reduce_norm(c, norm);
     }

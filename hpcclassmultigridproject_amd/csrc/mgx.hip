@@ -329,6 +329,12 @@ int op_vcycle(mgx_ctx *c, int l, double *norm, bool store_post) {
             CHK(op_smooth(c, 0, c->opt.nsmooth, false, /*restrict=*/true, false, nullptr));
         }
         CHK(op_vcycle(c, 1));
+        if (c->post_only) {   // the last cycle: prolongation + post-smoothing + norm only
+            bool fused = false;
+            CHK(op_smooth(c, 0, c->opt.nsmooth, /*prolong=*/true, false, /*norm=*/true, &fused));
+            L.spec = -1;
+            return fused ? read_norm(c, norm) : op_residual_norm(c, 0, norm);
+        }
         CHK(op_cross(c, store_post));
         return read_norm(c, norm);
     }
@@ -466,6 +472,20 @@ static int redo_post(mgx_ctx *c) {
     return dist_redo_post(c);
 }
 
+static void set_post_only(mgx_ctx *c, bool v) {
+    c->post_only = v;
+    if (c->dist)
+        for (int i = 0; i < dist_nsub(c); ++i) dist_sub(c, i)->post_only = v;
+}
+
+// tuning key "post_only": a cycle whose extrapolated norm is within tol /
+// post_only (or the last cycle mg_outer may run) skips the next cycle's
+// pre-smoothing: its finest level runs the post-smoothing pass alone, not the
+// cross pass (2.7 GB of u_pre + coarse rhs writes and B's sweeps saved); if it
+// does not converge after all, the next cycle pre-smooths from its u_post
+// (0 = never; -1 = every cycle, the test of that path)
+long g_post_only = 10;
+
 // tuning key "post_predict": mg_outer stores a cycle's u_post only when the
 // cycle is predicted to converge -- its norm extrapolated with the last
 // reduction factor within post_predict x tol -- and recomputes it in the
@@ -487,14 +507,21 @@ int op_mg_outer(mgx_ctx *c, double tol, int *cycles, double *res0_out, double *r
     const bool predict = g_post_predict != 0 && post_predictable(c);
     double prev = res0;
     for (; iter < c->opt.max_cycle && res / res0 > tol; ++iter) {
-        bool store = true;
-        if (predict && iter + 1 < c->opt.max_cycle) {   // the last allowed cycle always stores
+        bool store = true, last = false;
+        if (predict) {
             const double pred = res * (res / prev);
-            store = g_post_predict > 0 && pred <= g_post_predict * tol * res0;
+            if (iter + 1 < c->opt.max_cycle)   // the last allowed cycle always stores
+                store = g_post_predict > 0 && pred <= g_post_predict * tol * res0;
+            last = g_post_only < 0 ||
+                   (g_post_only > 0 && (iter + 1 == c->opt.max_cycle ||
+                                        pred * (double)g_post_only <= tol * res0));
         }
         prev = res;
-        CHK(cycle_norm(c, &res, store));
-        if (!store && !(res / res0 > tol)) CHK(redo_post(c));
+        set_post_only(c, last);
+        const int rc = cycle_norm(c, &res, store);
+        set_post_only(c, false);
+        CHK(rc);
+        if (!store && !last && !(res / res0 > tol)) CHK(redo_post(c));
     }
     if (cycles) *cycles = iter;
     if (res0_out) *res0_out = res0;
@@ -1098,6 +1125,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgx::set_xtile_max_rows(value);
         return MGX_OK;
     }
+    if (!strcmp(key, "post_only")) {
+        if (value < -1) return fail(MGX_E_ARG, "post_only must be >= -1");
+        mgxi::g_post_only = value;
+        return MGX_OK;
+    }
     if (!strcmp(key, "post_predict")) {
         if (value < -1) return fail(MGX_E_ARG, "post_predict must be >= -1");
         mgxi::g_post_predict = (double)value;
@@ -1161,6 +1193,10 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "xtile_max_rows")) {
         *value = mgx::get_xtile_max_rows();
+        return MGX_OK;
+    }
+    if (!strcmp(key, "post_only")) {
+        *value = mgxi::g_post_only;
         return MGX_OK;
     }
     if (!strcmp(key, "post_predict")) {

@@ -201,6 +201,11 @@ int mgx_synchronize(mgx_ctx *ctx);
  * within post_predict x tol; a cycle that converges without it is recomputed
  * by one post-smoothing pass (default 10; 0 = always store,
  * -1 = never store: bitwise the same results).
+ * "post_only": a cycle of mg_outer / step whose extrapolated norm is within
+ * tol / post_only (or the last cycle allowed) runs its finest post-smoothing
+ * as a pass of its own instead of the cross-cycle pass (no pre-smoothing of a
+ * next cycle that would not run); if it does not converge after all, the next
+ * cycle pre-smooths from its result (default 10; 0 = never; -1 = every cycle).
  * "coarse_lds": 1 (default) solves coarsest levels n <= 64 with the fields
  * in LDS, 0 = through L2 (bitwise the same).
  * None of them changes a result bit. */

@@ -261,21 +261,28 @@ def test_step_fused_rhs_norm_equals_rhs_then_mg_outer(N, G, fuse):
 def test_post_predict_recompute_is_bitwise(N, maxlvl, nsmooth, tol, G, min_rows):
     """mg_outer skips storing u_post on cycles predicted not to converge and
     recomputes it (prolongation + post-smoothing of the cycle's input) when
-    one converges anyway: post_predict -1 (never store, always recompute),
-    10 (the default prediction) and 0 (always store) give the same cycle
-    counts, norms and u, bitwise, over three time steps -- on one GPU and on
-    virtual row blocks."""
+    one converges anyway, and runs the cycle predicted to be the last as a
+    post-smoothing pass without the next cycle's pre-smoothing: post_predict
+    -1 (never store, always recompute), the defaults, post_only -1 (every
+    cycle post-only) and 0 / 0 (always the cross pass, always store) give the
+    same cycle counts and u, bitwise, and norms to 1e-11, over three time
+    steps -- on one GPU and on virtual row blocks."""
     dt = 1.0 / N / 10
     u0, v1, v2 = init_problem(N)
     old = _lib.get_tuning("post_predict")
+    old_po = _lib.get_tuning("post_only")
     old_rows = _lib.get_tuning("dist_min_rows")
     kw = dict(local_parts=G) if G > 1 else {}
     out = []
     try:
         if min_rows:
             _lib.set_tuning("dist_min_rows", min_rows)
-        for pp in (0, -1, 10):
+        # (post_predict, post_only): always store / never post-only first, then
+        # never store (recompute), the defaults, every cycle post-only (each
+        # next cycle pre-smooths from u_post)
+        for pp, po in ((0, 0), (-1, 0), (10, 10), (10, -1)):
             _lib.set_tuning("post_predict", pp)
+            _lib.set_tuning("post_only", po)
             with Multigrid(N, maxlvl, dt, NU, nsmooth=nsmooth, **kw) as mg:
                 if G > 1:
                     assert mg.dist_info()[2] == (0 if min_rows else 3)
@@ -288,7 +295,11 @@ def test_post_predict_recompute_is_bitwise(N, maxlvl, nsmooth, tol, G, min_rows)
                 out.append((res, mg.download()))
     finally:
         _lib.set_tuning("post_predict", old)
+        _lib.set_tuning("post_only", old_po)
         _lib.set_tuning("dist_min_rows", old_rows)
     for res, u in out[1:]:
-        assert res == out[0][0]
+        assert [r[0] for r in res[:2]] == [r[0] for r in out[0][0][:2]]
+        assert res[2] == out[0][0][2]
+        np.testing.assert_allclose(np.array([r[1:] for r in res[:2]]),
+                                   np.array([r[1:] for r in out[0][0][:2]]), rtol=1e-11)
         assert np.array_equal(u, out[0][1])
