@@ -208,7 +208,10 @@ int mgx_synchronize(mgx_ctx *ctx);
  * cycle pre-smooths from its result (default 10; 0 = never; -1 = every cycle).
  * "coarse_lds": 1 (default) solves coarsest levels n <= 64 with the fields
  * in LDS, 0 = through L2 (bitwise the same).
- * None of them changes a result bit. */
+ * None of them changes a bit of u or a cycle count; residual norms taken by
+ * a different kernel (cross_cycle, post_only, step_fuse) agree to 1e-11
+ * relative (other reduction trees; a cycle count could differ only on a norm
+ * that far from tol). */
 int mgx_set_tuning(const char *key, long value);
 int mgx_get_tuning(const char *key, long *value);
 
