@@ -39,6 +39,7 @@ struct Level {
     int xin = -1;   // finest level: the input buffer of the last cross-cycle pass
     int nxt() const { return cur == 0 ? 1 : 0; }   // ping-pong partner of cur
     double *rhs = nullptr, *v1 = nullptr, *v2 = nullptr;
+    double *rhs_alt = nullptr;   // finest level: the next time step's rhs (step mode)
     mgx::Coef coef{};
     double M() const { return double(n + 1) * double(n + 1); }
     double *U() const { return u[cur]; }
@@ -72,6 +73,12 @@ struct mgx_ctx {
     // mg_outer's cycle predicted to be the last: its finest level runs the
     // post-smoothing alone, not the cross pass (no next-cycle pre-smoothing)
     bool post_only = false;
+    // time-step mode: inside mgx_step (step_next) the last cycle's cross pass
+    // also forms the next step's rhs (lv[0].rhs_alt), initial norm
+    // (step_res0) and first pre-smoothing + restriction (lv[0].spec, lv[1]
+    // rhs); step_spec = that state is ready for the next mgx_step
+    bool step_next = false, step_spec = false;
+    double step_res0 = 0;
     // profiling
     int prof = 0;   // 0 off, 1 every launch, 2 finest-level launches only
     std::vector<mgxi::ProfRec> pending;

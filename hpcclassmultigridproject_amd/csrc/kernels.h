@@ -111,8 +111,14 @@ struct XArgs {
     bool norm_accumulate = false;   // *norm_out += sum of squares (split pass)
     int ra = 0, rb = -1, lo = 0, hi = -1;   // row block (rb < 0: whole level), as SmoothArgs
     int min_rows = 64;   // fewest rows per workgroup (short bands: smaller, more parallel)
+    // time-step mode (whole level, one GPU): B's pre-smoothing is the next time
+    // step's, with its rhs formed from u_post into rhs_next and its initial
+    // norm into *norm2_out; partials needs 2 * norm_partials_size() doubles
+    double *rhs_next = nullptr, *norm2_out = nullptr;
 };
 int launch_xsmooth(const XArgs &a, int sweeps, hipStream_t s);
+// whether launch_xsmooth supports rhs_next on a whole level of size n
+bool xstep_supported(long n);
 // Cross pass: 1 = interior strips run the unguarded march (default), 0 = all guarded.
 void set_xfast(long v);
 long get_xfast();

@@ -1000,6 +1000,11 @@ struct XCfg {
     // in [1, n-1] so that no update ever lands on a Dirichlet row.
     // (+1: the march runs an even number of steps)
     static constexpr int TOP = EA + EB + NR + D + S + 2, BOT = D + EB + NR + 7;
+    // step mode (RS): B's march has one more stage in front (the next time
+    // step's rhs from u_post), so A starts one row earlier: 2 more margin rows
+    // (even) for the unguarded form; the halo H is unchanged (S + EB + 1 =
+    // 14 columns fit its 7 pairs)
+    static constexpr int TOP_RS = TOP + 2;
 };
 
 
@@ -1011,13 +1016,23 @@ struct XCfg {
 // no exec-mask branches, -26 % instructions.  They are separate kernels: one
 // function holding both marches compiled to a worse schedule than either
 // (3.6 ms vs 2.7 ms unguarded / 3.1 ms guarded at N=16384).
-template <int WPB, int K, bool G>
+//
+// RS = true (time-step mode, mg_outer's last cycle of a time step whose next
+// step follows): B's pre-smoothing is the NEXT time step's first one.  B
+// forms the next step's rhs of each row from the final u_post rows as they
+// arrive (gs.cpp:44, the expressions of rhs_point_t), stores it to rhs_next,
+// sums the residual of u_post against it (the next mg_outer's initial norm,
+// multigrid.cpp:104) into partials2, and smooths and restricts with it --
+// the rhs + norm pass of the next step and this step's post-smoothing pass
+// in one HBM pass.  (B's half of the u_post norm still uses this step's rhs.)
+template <int WPB, int K, bool G, bool RS = false>
 __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     const double *__restrict__ uin, double *__restrict__ upost, double *__restrict__ upre,
     const double *__restrict__ rhs, const double *__restrict__ v1, const double *__restrict__ v2,
     const double *__restrict__ uc, long pitchc, double *__restrict__ rhsc,
     double *__restrict__ partials, int n, long pitch, MarchRegions reg, long units_per_wg, Coef c,
-    int lo, int hi, int store_post) {
+    int lo, int hi, int store_post, double *__restrict__ rhs_next,
+    double *__restrict__ partials2) {
     using X = XCfg<K>;
     constexpr int S = X::S, H = X::H, NR = X::NR, W = X::W, D = X::D, NU = X::NU,
                   NRD = X::NRD, EA = X::EA, EB = X::EB;
@@ -1044,7 +1059,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     march_units(reg, WPB, units_per_wg, start, end);
     const int nc = n >> 1;
     const double hh = c.h * 0.5;
-    double acc = 0.0;
+    double acc = 0.0, acc2 = 0.0;
 
     // One march of the pair over owned rows [a, b) of strip j0 (G: see above;
     // the unguarded form keeps only the uniform owned-row tests of its outputs)
@@ -1136,7 +1151,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
         // A's first step (aligned to NR so ring indices and parities are
         // static); B runs D steps behind; the last iteration is B's last step
         // (rounded up to whole pairs: an extra step stores nothing)
-        int s0 = a - EB - EA;
+        int s0 = a - EB - EA - (RS ? 1 : 0);
         s0 = s0 >= 0 ? (s0 / NR) * NR : -(((-s0) + NR - 1) / NR) * NR;
         s0 = __builtin_amdgcn_readfirstlane(s0);
         const int iters = ((b + EB - 3) + D - s0 + 1 + 1) & ~1;
@@ -1301,6 +1316,42 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                             acc += (keep && rin) ? r1 * r1 : 0.0;
                         }
                     }
+                    if (RS) {
+                        // the next step's rhs of row s+2 from u_post rows s+1..s+3
+                        // (gs.cpp:44), stored on the owned interior points, and the
+                        // residual of u_post against it (multigrid.cpp:104); it
+                        // replaces this step's rhs in the ring for B's stages and
+                        // restriction
+                        const int r = s + 2;
+                        const int iR = (q + 2) % NR, iN = (q + 1) % NR, iS = (q + 3) % NR;
+                        RowData &d = rd[iR];
+                        const double uW = dpp_shr1(ur[iR].y), uE = dpp_shl1(ur[iR].x);
+                        Coef cg = c;   // fresh nu: no coefficient CSE into the stages
+                        asm volatile("" : "+s"(cg.nu));
+                        const double f0 = rhs_point_t(d.x.x, d.y.x, ur[iR].x, ur[iN].x, uW,
+                                                      ur[iS].x, ur[iR].y, cg);
+                        const double f1 = rhs_point_t(d.x.y, d.y.y, ur[iR].y, ur[iN].y, ur[iR].x,
+                                                      ur[iS].y, uE, cg);
+                        d.r = make_double2(f0, f1);
+                        const bool rin = r >= a && r < b;
+                        const bool i0 = !GN || (r >= 1 && r <= n - 1 && in0);
+                        const bool i1 = !GN || (r >= 1 && r <= n - 1 && in1);
+                        double *row = rhs_next + (long)r * pitch;
+                        if (rin && keep) {
+                            if (i0 && i1) {
+                                st2s(row + c0, d.r);
+                            } else {
+                                if (i0) row[c0] = f0;
+                                if (i1) row[c0 + 1] = f1;
+                            }
+                        }
+                        const double e0 = res_point_t(f0, d.x.x, d.y.x, ur[iR].x, ur[iN].x, uW,
+                                                      ur[iS].x, ur[iR].y, cg);
+                        const double e1 = res_point_t(f1, d.x.y, d.y.y, ur[iR].y, ur[iN].y,
+                                                      ur[iR].x, ur[iS].y, uE, cg);
+                        acc2 += (rin && keep && i0) ? e0 * e0 : 0.0;
+                        acc2 += (rin && keep && i1) ? e1 * e1 : 0.0;
+                    }
                     to_coef(rd[(q + 1) % NR], cf[(q + 1) % NR]);   // row s+1
 #pragma unroll
                     for (int h = 0; h < S; ++h) stage_c(q, h, s + 1 - h);
@@ -1342,6 +1393,10 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     }
     const double tot = wave_sum(acc);   // one partial per wave (A: columns c0, B: c0+1)
     if (l == 0) partials[(long)blockIdx.x * 2 * WPB + wv] = tot;
+    if (RS) {
+        const double tot2 = wave_sum(acc2);   // B only (A's are +0)
+        if (l == 0) partials2[(long)blockIdx.x * 2 * WPB + wv] = tot2;
+    }
 }
 
 // k_smooth_tile: the same fused pass (K sweeps + optional prolong / restrict
@@ -2290,15 +2345,15 @@ static int smooth_winst(const SmoothArgs &A, hipStream_t s) {
 }
 
 
-template <int WPB, int K, bool G>
+template <int WPB, int K, bool G, bool RS = false>
 static int xsmooth_slots() {
     static int slots = 0;   // resident workgroups of this instantiation
     if (!slots) {
         int dev = 0, cus = 0, per = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_xsmooth<WPB, K, G>, 128 * WPB,
-                                                           0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_xsmooth<WPB, K, G, RS>,
+                                                           128 * WPB, 0);
         slots = std::max(1, cus) * std::max(1, per);
     }
     return slots;
@@ -2307,7 +2362,7 @@ static int xsmooth_slots() {
 // One launch over `reg`; min_rows: the fewest rows per workgroup (each
 // workgroup's march pays a warm-up of ~EA + EB + D rows).  Returns the norm
 // partials written (grid * 2 * WPB: one per wave) at `partials`.
-template <int WPB, int K, bool G>
+template <int WPB, int K, bool G, bool RS = false>
 static int xsmooth_launch(const XArgs &A, const MarchRegions &reg, double *partials, int lo, int hi,
                           long min_rows, long max_wgs, hipStream_t s) {
     const long total = reg.pre[reg.count];
@@ -2315,11 +2370,14 @@ static int xsmooth_launch(const XArgs &A, const MarchRegions &reg, double *parti
     long upw;
     MarchRegions r;
     using X = XCfg<K>;
-    const unsigned grid = plan_march(reg, WPB, xsmooth_slots<WPB, K, G>(), min_rows, max_wgs,
+    const unsigned grid = plan_march(reg, WPB, xsmooth_slots<WPB, K, G, RS>(), min_rows, max_wgs,
                                      X::EA + X::EB + X::D + X::NR / 2, upw, r);
-    MGX_LAUNCH((k_xsmooth<WPB, K, G>), dim3(grid), dim3(128 * WPB), s, A.uin, A.upost, A.upre,
-               A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch, r, upw,
-               A.c, lo, hi, A.store_post ? 1 : 0);
+    // RS: the second partials (the next step's initial norm) at the same
+    // offsets, kNormBlocks further on
+    MGX_LAUNCH((k_xsmooth<WPB, K, G, RS>), dim3(grid), dim3(128 * WPB), s, A.uin, A.upost,
+               A.upre, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch, r,
+               upw, A.c, lo, hi, A.store_post ? 1 : 0, A.rhs_next,
+               RS ? partials + kNormBlocks : (double *)nullptr);
     return (int)grid * 2 * WPB;
 }
 
@@ -2396,6 +2454,22 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
         lo = 0;
         hi = (int)n;
     }
+    if (A.rhs_next) {
+        // time-step mode: whole levels on one GPU with the split launches only
+        // (the caller checks xstep_supported first)
+        if (g_xfast == 0 || !(A.c.dgs > 0) || A.rb >= 0 || rb - ra <= g_xtile_max_rows)
+            return -3;
+        MarchRegions inner, edge, unused;
+        march_regions<WPB>(n, X::W, X::H, ra, rb, X::TOP_RS, X::BOT, true, inner, unused);
+        march_regions<1>(n, X::W, X::H, ra, rb, X::TOP_RS, X::BOT, true, unused, edge);
+        const int pm = xsmooth_launch<WPB, K, false, true>(A, inner, A.partials, lo, hi,
+                                                           A.min_rows, kNormBlocks / (2 * WPB) / 2,
+                                                           s);
+        const int pe = xsmooth_launch<1, K, true, true>(A, edge, A.partials + pm, lo, hi,
+                                                        std::min(32, A.min_rows),
+                                                        kNormBlocks / 2 / 2, s);
+        return pm + pe;
+    }
     // inner: WPB pairs per workgroup, one workgroup per CU, long segments;
     // edge: one pair per workgroup (4 per CU) and short segments, so that its
     // ~44 K strip-rows at N=16384 (2 boundary strips + 71-row bands) take
@@ -2430,7 +2504,14 @@ int launch_xsmooth(const XArgs &A, int sweeps, hipStream_t s) {
     if (blocks > 0)
         MGX_LAUNCH(k_norm_final, dim3(1), dim3(kFinalThreads), s, (const double *)A.partials,
                    blocks, A.norm_out, A.norm_accumulate ? 2 : A.norm_sqrt ? 1 : 0);
+    if (blocks > 0 && A.rhs_next)   // the next step's initial norm
+        MGX_LAUNCH(k_norm_final, dim3(1), dim3(kFinalThreads), s,
+                   (const double *)(A.partials + kNormBlocks), blocks, A.norm2_out, 1);
     return blocks;
+}
+
+bool xstep_supported(long n) {
+    return g_xfast != 0 && n + 1 > g_xtile_max_rows;
 }
 
 long g_tile_max_n = -1;   // levels with n <= this use k_smooth_tile

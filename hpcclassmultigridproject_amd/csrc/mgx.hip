@@ -263,15 +263,21 @@ static bool cross_ok(mgx_ctx *c) {
 // touches the levels; every other mutating entry point drops it.
 void drop_spec(mgx_ctx *c) {
     if (!c->lv.empty()) c->lv[0].spec = -1;
+    c->step_spec = false;
 }
 
 // k_xsmooth on level 0: u_post (cycle k, returned by mg_outer if it stops
 // here) into one free buffer, u_pre (cycle k+1's pre-smoothing) into the
 // other, the residual of u_post -> c->dscal[0], the restriction of u_pre's
 // residual -> rhs[1] (u[1] flagged zero for cycle k+1).
-static int op_cross(mgx_ctx *c, bool store_post) {
+static int op_cross(mgx_ctx *c, bool store_post, bool rs = false) {
     Level &L = c->lv[0], &Cl = c->lv[1];
     CHK(materialize(c, 1));
+    if (rs && !L.rhs_alt) {   // zero boundary: compute_rhs writes the interior only
+        const size_t bytes = sizeof(double) * (size_t)(L.n + 1) * (size_t)L.pitch;
+        HIPCHK(hipMalloc(&L.rhs_alt, bytes));
+        HIPCHK(hipMemsetAsync(L.rhs_alt, 0, bytes, c->stream));
+    }
     int P = -1, Q = -1;
     for (int i = 0; i < 3; ++i)
         if (i != L.cur) (P < 0 ? P : Q) = i;
@@ -291,6 +297,10 @@ static int op_cross(mgx_ctx *c, bool store_post) {
     A.pitch = L.pitch;
     A.c = L.coef;
     A.store_post = store_post;
+    if (rs) {
+        A.rhs_next = L.rhs_alt;
+        A.norm2_out = c->dscal + 6;
+    }
     const int k = c->opt.nsmooth;
     // algorithmic bytes: prolong+add, k sweeps, residual+norm (post of cycle
     // k) + k sweeps, residual+restriction (pre of cycle k+1), SURVEY 8d
@@ -298,11 +308,15 @@ static int op_cross(mgx_ctx *c, bool store_post) {
                          (40.0 * k + 40.0) * L.M() + 24.0 * Cl.M();
     // compulsory: u, rhs, v1, v2 and the coarse u read once; u_pre (+ u_post)
     // and the coarse rhs written once
-    const double cbytes = 8.0 * ((store_post ? 6.0 : 5.0) * L.M() + 2.0 * Cl.M());
+    // (step mode: + compute_rhs and the initial residual norm of the next
+    // step, and its rhs written)
+    const double bytes_rs = rs ? (32.0 + 48.0) * L.M() : 0.0;
+    const double cbytes =
+        8.0 * ((store_post ? 6.0 : 5.0) * L.M() + 2.0 * Cl.M() + (rs ? L.M() : 0.0));
     int blocks = 0;
-    CHK(launch(c, MGX_K_XSMOOTH, 0, bytes, cbytes,
+    CHK(launch(c, MGX_K_XSMOOTH, 0, bytes + bytes_rs, cbytes,
                [&] { blocks = mgx::launch_xsmooth(A, k, c->stream); }));
-    if (blocks < 0) return fail(MGX_E_ARG, "launch_xsmooth: unsupported sweeps");
+    if (blocks < 0) return fail(MGX_E_ARG, "launch_xsmooth: unsupported sweeps / mode");
     L.xin = L.cur;
     L.cur = P;
     L.spec = Q;
@@ -329,6 +343,20 @@ int op_vcycle(mgx_ctx *c, int l, double *norm, bool store_post) {
             CHK(op_smooth(c, 0, c->opt.nsmooth, false, /*restrict=*/true, false, nullptr));
         }
         CHK(op_vcycle(c, 1));
+        if (c->post_only && c->step_next && mgx::xstep_supported(L.n) && L.coef.dgs > 0) {
+            // the last cycle of a time step whose next step follows: the cross
+            // pass in step mode (u_post stored; B pre-smooths the next step)
+            CHK(op_cross(c, /*store_post=*/true, /*rs=*/true));
+            HIPCHK(hipMemcpyAsync(c->hscal, c->dscal, sizeof(double), hipMemcpyDeviceToHost,
+                                  c->stream));
+            HIPCHK(hipMemcpyAsync(c->hscal + 6, c->dscal + 6, sizeof(double),
+                                  hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            *norm = c->hscal[0];
+            c->step_res0 = c->hscal[6];
+            c->step_spec = true;
+            return MGX_OK;
+        }
         if (c->post_only) {   // the last cycle: prolongation + post-smoothing + norm only
             bool fused = false;
             CHK(op_smooth(c, 0, c->opt.nsmooth, /*prolong=*/true, false, /*norm=*/true, &fused));
@@ -521,6 +549,12 @@ int op_mg_outer(mgx_ctx *c, double tol, int *cycles, double *res0_out, double *r
         const int rc = cycle_norm(c, &res, store);
         set_post_only(c, false);
         CHK(rc);
+        if (c->step_spec && res / res0 > tol) {
+            // step mode, but the cycle did not converge: its pre-smoothing was
+            // the next step's (other rhs); the next cycle pre-smooths from u_post
+            c->step_spec = false;
+            c->lv[0].spec = -1;
+        }
         if (!store && !last && !(res / res0 > tol)) CHK(redo_post(c));
     }
     if (cycles) *cycles = iter;
@@ -580,6 +614,7 @@ void free_ctx(mgx_ctx *c) {
         (void)hipFree(L.u[1]);
         (void)hipFree(L.u[2]);
         (void)hipFree(L.rhs);
+        (void)hipFree(L.rhs_alt);
         (void)hipFree(L.v1);
         (void)hipFree(L.v2);
     }
@@ -742,7 +777,8 @@ int mgxi::create_ctx(mgx_ctx **out, long n, int maxlvl, double dt, double nu,
             return bail(fail(MGX_E_HIP, "hipMalloc (level tower): out of device memory"));
     }
     const size_t flat = sizeof(double) * (n + 1) * (n + 1);
-    if (hipMalloc(&c->partials, sizeof(double) * mgx::norm_partials_size()) != hipSuccess ||
+    // (two partial arrays: the cross pass's time-step mode sums two norms)
+    if (hipMalloc(&c->partials, 2 * sizeof(double) * mgx::norm_partials_size()) != hipSuccess ||
         hipMalloc(&c->dscal, sizeof(double) * 8) != hipSuccess ||
         hipHostMalloc(&c->hscal, sizeof(double) * 8) != hipSuccess)
         return bail(fail(MGX_E_HIP, "hipMalloc (scratch)"));
@@ -779,6 +815,7 @@ int mgxi::upload_ctx(mgx_ctx *c, const double *u0, const double *v1, const doubl
     L.cur = 0;
     L.zero = false;
     L.spec = -1;
+    c->step_spec = false;   // a pending next-step state belongs to the old fields
     const double *src[3] = {u0, v1, v2};
     double *dst[3] = {L.u[0], L.v1, L.v2};
     for (int k = 0; k < 3; ++k)
@@ -866,30 +903,56 @@ int mgx_prolong_add(mgx_ctx *c, int level) {
     drop_spec(c);
     return op_prolong_add(c, level);
 }
+// A pending next-step state (mgx_step) is only valid for the next mgx_step.
+static void drop_step_spec(mgx_ctx *c) {
+    if (c->step_spec) drop_spec(c);
+}
 int mgx_vcycle(mgx_ctx *c) {
     if (!c) return fail(MGX_E_ARG, "null ctx");
+    drop_step_spec(c);
     if (c->dist) return dist_vcycle(c, nullptr);
     return op_vcycle(c, 0);
 }
 int mgx_mg_outer(mgx_ctx *c, double tol, int *cycles, double *res0, double *res) {
     if (!c) return fail(MGX_E_ARG, "null ctx");
+    drop_step_spec(c);
     return op_mg_outer(c, tol, cycles, res0, res);
+}
+// tuning key "step_cross": 1 (default) = mgx_step's last cycle also forms the
+// next step's rhs, initial norm and first pre-smoothing (cross pass in step
+// mode), consumed by the next mgx_step; 0 = each step starts with its own
+// rhs + norm pass
+long g_step_cross = 1;
+
+static int step_impl(mgx_ctx *c, double tol, int *cycles, bool prepare_next) {
+    // compute_rhs and mg_outer's initial norm in one pass (timestepper,
+    // multigrid.cpp:168-170), with the first pre-smoothing where it fuses --
+    // or already done by the previous step's last cross pass
+    double res0 = 0;
+    if (c->step_spec && !c->dist) {
+        Level &L = c->lv[0];
+        std::swap(L.rhs, L.rhs_alt);
+        res0 = c->step_res0;
+        c->step_spec = false;   // lv[0].spec and lv[1]'s rhs stay: the first cycle's
+    } else if (c->dist) {
+        CHK(dist_rhs_norm(c, &res0));
+    } else if (step_fusable(c)) {
+        CHK(op_rhs_norm_pre(c, &res0));
+    } else {
+        CHK(op_rhs_norm(c, &res0));
+    }
+    c->step_next = prepare_next && g_step_cross != 0 && !c->dist;
+    const int rc = op_mg_outer(c, tol, cycles, nullptr, nullptr, &res0);
+    c->step_next = false;
+    return rc;
 }
 int mgx_step(mgx_ctx *c, double tol, int *cycles) {
     if (!c) return fail(MGX_E_ARG, "null ctx");
-    // compute_rhs and mg_outer's initial norm in one pass (timestepper,
-    // multigrid.cpp:168-170), with the first pre-smoothing where it fuses
-    double res0 = 0;
-    if (c->dist)
-        CHK(dist_rhs_norm(c, &res0));
-    else if (step_fusable(c))
-        CHK(op_rhs_norm_pre(c, &res0));
-    else
-        CHK(op_rhs_norm(c, &res0));
-    return op_mg_outer(c, tol, cycles, nullptr, nullptr, &res0);
+    return step_impl(c, tol, cycles, true);
 }
 int mgx_run_cycles(mgx_ctx *c, int cycles, double *res) {
     if (!c || cycles < 0) return fail(MGX_E_ARG, "mgx_run_cycles: bad args");
+    drop_step_spec(c);
     double r = 0;
     for (int k = 0; k < cycles; ++k) CHK(cycle_norm(c, &r, /*store_post=*/k == cycles - 1));
     if (res) *res = r;
@@ -991,7 +1054,7 @@ int mgx_timestepper_ex(double *uT, const double *u0, const double *v1, const dou
     const int steps = (int)(T / dt);   // multigrid.cpp:165
     for (int it = 0; rc == MGX_OK && it < steps; ++it) {
         int cyc = 0;
-        rc = mgx_step(c, tol, &cyc);
+        rc = step_impl(c, tol, &cyc, /*prepare_next=*/it + 1 < steps);
         if (rc == MGX_E_NOCONV) {
             // multigrid.cpp:117-119 only warns; keep stepping
             printf("multigrid did not converge in %d cycles\n", c->opt.max_cycle);
@@ -1125,6 +1188,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgx::set_xtile_max_rows(value);
         return MGX_OK;
     }
+    if (!strcmp(key, "step_cross")) {
+        if (value != 0 && value != 1) return fail(MGX_E_ARG, "step_cross must be 0 or 1");
+        g_step_cross = value;
+        return MGX_OK;
+    }
     if (!strcmp(key, "post_only")) {
         if (value < -1) return fail(MGX_E_ARG, "post_only must be >= -1");
         mgxi::g_post_only = value;
@@ -1193,6 +1261,10 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "xtile_max_rows")) {
         *value = mgx::get_xtile_max_rows();
+        return MGX_OK;
+    }
+    if (!strcmp(key, "step_cross")) {
+        *value = g_step_cross;
         return MGX_OK;
     }
     if (!strcmp(key, "post_only")) {

@@ -206,6 +206,11 @@ int mgx_synchronize(mgx_ctx *ctx);
  * as a pass of its own instead of the cross-cycle pass (no pre-smoothing of a
  * next cycle that would not run); if it does not converge after all, the next
  * cycle pre-smooths from its result (default 10; 0 = never; -1 = every cycle).
+ * "step_cross": 1 (default) lets mgx_step's last cycle (single GPU, whole
+ * levels n >= 8192) run the cross-cycle pass in time-step mode: it also
+ * forms the next step's rhs, initial norm and first pre-smoothing, which the
+ * next mgx_step starts from (any other call in between drops them); 0 = each
+ * step starts with its own rhs + norm pass.
  * "coarse_lds": 1 (default) solves coarsest levels n <= 64 with the fields
  * in LDS, 0 = through L2 (bitwise the same).
  * None of them changes a bit of u or a cycle count; residual norms taken by

@@ -303,3 +303,67 @@ def test_post_predict_recompute_is_bitwise(N, maxlvl, nsmooth, tol, G, min_rows)
         np.testing.assert_allclose(np.array([r[1:] for r in res[:2]]),
                                    np.array([r[1:] for r in out[0][0][:2]]), rtol=1e-11)
         assert np.array_equal(u, out[0][1])
+
+
+@pytest.mark.parametrize("post_only", [10, -1], ids=["default", "every_cycle"])
+def test_step_cross_prepares_next_step_bitwise(post_only):
+    """mgx_step's last cycle runs the cross pass in time-step mode: wave B
+    forms the NEXT step's rhs from u_post, its initial norm, its first
+    pre-smoothing and restriction, and the next mgx_step starts from that
+    (step_cross = 1) -- against each step's own rhs + norm pass (0): the same
+    cycle counts and u bitwise over four steps, the rhs of the last step
+    bitwise; post_only = -1 runs step mode on every cycle, so every cycle but
+    the last of a step mispredicts and falls back (pre-smoothing from u_post
+    with the step's own rhs)."""
+    N, L = 8192, 6
+    dt, tol = 1.0 / N / 10, 1e-6
+    u0, v1, v2 = init_problem(N)
+    old = {k: _lib.get_tuning(k) for k in ("step_cross", "post_only")}
+    out = []
+    try:
+        _lib.set_tuning("post_only", post_only)
+        for sc in (0, 1):
+            _lib.set_tuning("step_cross", sc)
+            with Multigrid(N, L, dt, NU) as mg:
+                mg.upload(u0, v1, v2)
+                mg.profile(True, finest_only=True)
+                cyc = [mg.step(tol) for _ in range(4)]
+                rhs_passes = mg.profile_get(_lib.K_RHS, 0)[0]
+                mg.profile(False)
+                out.append((cyc, mg.download(), mg.download_level(0, "rhs"), rhs_passes))
+    finally:
+        for k, v in old.items():
+            _lib.set_tuning(k, v)
+    (c0, u0_, r0_, n0), (c1, u1_, r1_, n1) = out
+    assert c0 == c1
+    assert np.array_equal(u0_, u1_) and np.array_equal(r0_, r1_)
+    assert n0 == 4 and n1 == 1   # one rhs + norm pass, the first step's
+
+
+def test_step_cross_state_dropped_by_other_calls():
+    """The next-step state a step leaves is used only by the next mgx_step:
+    an upload, rhs + mg_outer or run_cycles in between drop it (each gives
+    what it gives on a fresh context)."""
+    N, L = 8192, 6
+    dt, tol = 1.0 / N / 10, 1e-6
+    u0, v1, v2 = init_problem(N)
+    with Multigrid(N, L, dt, NU) as fresh:
+        fresh.upload(u0, v1, v2)
+        ref_step = [fresh.step(tol) for _ in range(2)]
+        ref_u = fresh.download()
+        fresh.upload(u0, v1, v2)
+        fresh.rhs()
+        ref_outer = fresh.mg_outer(tol)[0]
+        ref_outer_u = fresh.download()
+    with Multigrid(N, L, dt, NU) as mg:
+        mg.upload(u0, v1, v2)
+        mg.step(tol)                      # leaves the next step's state
+        mg.upload(u0, v1, v2)             # ... which the upload drops
+        assert [mg.step(tol) for _ in range(2)] == ref_step
+        assert np.array_equal(mg.download(), ref_u)
+        mg.upload(u0, v1, v2)
+        mg.step(tol)
+        mg.upload(u0, v1, v2)
+        mg.rhs()
+        assert mg.mg_outer(tol)[0] == ref_outer
+        assert np.array_equal(mg.download(), ref_outer_u)
