@@ -34,11 +34,12 @@ def test_multigrid_driver_writes_reference_uT(tmp_path):
         with open(tmp_path / name) as f:
             assert f.read() == want, name
     # the reference's line shapes (multigrid.cpp:246, :259, :266):
-    # "\n<label> time, N = %i: %f s\n" twice, then the %10e error line
+    # exactly, labels included, then the %10e error line
     lines = out.split("\n")
     timed = [l for l in lines if re.fullmatch(r".+ time, N = 32: \d+\.\d{6} s", l)]
     assert len(timed) == 2, out
-    assert timed[0].startswith("GPU (1 MI355X") and timed[1].startswith("GPU with ")
+    assert re.fullmatch(r"CPU \(1 thread for reference\) time, N = 32: \d+\.\d{6} s", timed[0])
+    assert re.fullmatch(r"CPU with OMP \(\d+ threads\) time, N = 32: \d+\.\d{6} s", timed[1])
     assert lines[lines.index(timed[0]) - 1] == "" and lines[lines.index(timed[1]) - 1] == ""
     assert "Error (compared to the referenced solution) = 0.000000e+00" in lines
 
