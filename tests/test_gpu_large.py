@@ -160,3 +160,53 @@ def test_fused_context_pass_N65536(oracle_mod):
         assert np.array_equal(got[a * W:e * W], want[a * W:e * W]), r0
     del u, u0
     _free()
+
+
+def test_C5_vcycles_N65536_one_gpu_equal_eight_row_blocks():
+    """Config C5's whole solver at its size: N = 65536, L = 11 (coarsest 64),
+    two V-cycles of mg_outer's pattern (cross-cycle finest pass, residual
+    norms) on one GPU, and the same on the C5 partition -- 8 row blocks with
+    row-block upload (each block initialised from its own rows only, the
+    correct velocity tower built on the device), the exchanges as device
+    copies (virtual ranks: the plan the 8 RCCL ranks execute).  The finest
+    field is BITWISE the same, norms to the summation-order tolerance.  No
+    CPU answer exists at this size; the one-GPU path is pinned to the
+    reference at N <= 16384 (test_gpu_solver) and the partitioned path to it
+    at C4 (test_gpu_dist), so this checks that both stay one computation past
+    2^32 points.  ~265 GB of HBM for the one-GPU towers."""
+    from hpcclassmultigridproject_amd import init_problem_rows
+    import time
+    free, _ = torch.cuda.mem_get_info()
+    if free < 272e9:
+        pytest.skip(f"needs ~270 GB of free HBM, {free / 1e9:.0f} GB free")
+    L = 11
+    u0, v1, v2 = init_problem(N, nthreads=16)
+    with Multigrid(N, L, K_DT, NU, tower_mode=_lib.TOWER_CORRECT) as mg:
+        mg.upload(u0, v1, v2)
+        del v1, v2
+        mg.rhs()
+        mg.synchronize()
+        t0 = time.perf_counter()
+        n_ref = [mg.run_cycles(1) for _ in range(2)]
+        dt = (time.perf_counter() - t0) / 2
+        u_ref = mg.download(u0)
+    print(f"\nN=65536 L=11 one GPU: {dt * 1e3:.1f} ms per V-cycle (incl. its norm), "
+          f"{(N - 1) ** 2 / dt:.3e} grid-point updates/s; norms {n_ref}", flush=True)
+    _free()
+    with Multigrid(N, L, K_DT, NU, tower_mode=_lib.TOWER_CORRECT, local_parts=8) as mg:
+        assert mg.dist_info()[0] == 8
+        blocks = []
+        for part in range(8):
+            lo, hi = mg.dist_rows(part)
+            blocks.append(init_problem_rows(N, lo, hi + 1, nthreads=16))
+        mg.upload_rows(blocks)
+        del blocks
+        mg.rhs()
+        n_got = [mg.run_cycles(1) for _ in range(2)]
+        got = mg.download()
+    try:
+        assert np.array_equal(got, u_ref)
+    finally:
+        del got, u_ref
+        _free()
+    np.testing.assert_allclose(n_got, n_ref, rtol=NORM_RTOL)
