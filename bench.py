@@ -297,7 +297,11 @@ def main():
     # the correct velocity tower (the reference tower reads the whole grid)
     row_upload = world > 1 and (args.row_upload == "on" or
                                 (args.row_upload == "auto" and N > 16384))
-    tower = pkg._lib.TOWER_CORRECT if row_upload else pkg._lib.TOWER_REFERENCE
+    # (and above N=16384 everywhere: the reference tower's two whole-grid
+    # staging buffers, 2 x 34 GB at N=65536, do not fit beside the towers on
+    # one GPU; the reference's own int indexing overflows there)
+    tower = (pkg._lib.TOWER_CORRECT if row_upload or N > 16384
+             else pkg._lib.TOWER_REFERENCE)
     mg = pkg.Multigrid(N, L, dt, nu, nsmooth=args.nsmooth, device=local,
                        smoother=args.smoother, fuse=args.fuse, tower_mode=tower, **dist_kw)
     la = mg.dist_info()[2]
@@ -424,7 +428,8 @@ def main():
         "config": {"workload": f"N={N} fp64 V-cycle, L={L} (coarsest {N >> (L - 1)}), "
                                f"nu_smooth={args.nsmooth}, + residual/norm per step",
                    "N": N, "levels": L, "nsmooth": args.nsmooth,
-                   "tower": "correct (row-block upload)" if row_upload else "reference",
+                   "tower": ("correct (row-block upload)" if row_upload else
+                             "correct" if tower == pkg._lib.TOWER_CORRECT else "reference"),
                    "parallelism": (f"row-partition x{world} on levels 0..{la - 1}, "
                                    f"levels {la}..{L - 1} replicated" if world > 1
                                    else "single"),
