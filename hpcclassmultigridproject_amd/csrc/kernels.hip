@@ -428,13 +428,14 @@ __global__ __launch_bounds__(BLOCK) void k_gs_sweep(const double *__restrict__ u
 #undef MGX_GS_STEP
 }
 
-// k_smooth: K red-black sweeps in ONE pass over HBM (temporal blocking).
+// Temporal blocking, shared by the row marches (k_wsmooth, k_xsmooth) and
+// the LDS tiles (k_smooth_tile): K red-black sweeps in ONE pass over HBM.
 //
 // The 2K half-sweeps are "stages" h = 0..S-1 (S = 2K; even h red, odd h
-// black).  A workgroup marches down the rows of a strip; at step s stage h
+// black).  A march goes down the rows of a strip; at step s stage h
 // updates its colour in row s+1-h, reading the other colour of rows
-// s-h..s+2-h as left by stage h-1.  One barrier separates consecutive stages.
-// u rows live in an LDS ring; each lane owns one column pair (2c, 2c+1).
+// s-h..s+2-h as left by stage h-1.  Each lane owns one column pair
+// (2c, 2c+1).
 // Optional last stage h = S (RESTRICT / NORM): the residual of row s+1-S,
 // whose neighbours are final by then.
 //
@@ -448,12 +449,11 @@ __global__ __launch_bounds__(BLOCK) void k_gs_sweep(const double *__restrict__ u
 // bitwise that of K reference sweeps.
 //
 // rhs / v1 / v2 of a row stay in registers from the step they are loaded to
-// the last stage that needs them; they are loaded two steps before their
-// first use into the one ring slot that dies each step, and u rows are
-// prefetched two steps ahead too (two alternating register sets).  The step loop is unrolled by NS = S+2
-// (even), and its start aligned to NS, so every register-ring index and the
-// parity of every row are compile-time constants: no selects, static LDS
-// offsets.  Ring slots are scalar (SALU) arithmetic.
+// the last stage that needs them, in the ring slot that dies each step; u
+// rows are prefetched ahead too (two alternating register sets).  The step
+// loop is unrolled by the (even) ring period and its start aligned to it, so
+// every register-ring index and the parity of every row are compile-time
+// constants: no selects, static LDS offsets.
 //
 // Division by the diagonal 1-4*rr*nu uses the host-computed y = RN(1/d) and
 // one Markstein correction: q0 = a*y, r = fma(-q0,d,a), q = fma(r,y,q0)
@@ -468,8 +468,8 @@ __global__ __launch_bounds__(BLOCK) void k_gs_sweep(const double *__restrict__ u
 // rhs, multigrid.cpp:73-75 fused); 8 NORM (sum of squared residuals of the
 // interior: per-workgroup partials, multigrid.cpp:112-113 fused).
 //
-// Work split: a 1-D grid of G workgroups, each gets an equal share of the
-// strip-major (strip, row) space, so one launch is one balanced wave.
+// Work split (marches): a 1-D grid of workgroups, each with a share of the
+// (strip, row) space (MarchRegions below), so one launch is one balanced wave.
 struct RowData {
     double2 r, x, y;
 };
@@ -600,7 +600,7 @@ __device__ __forceinline__ void march_units(const MarchRegions &reg, int wpb, lo
     end = start + h;
 }
 
-// k_wsmooth: the fused K-sweep pass of k_smooth as a WAVE-PRIVATE march.
+// k_wsmooth: the fused K-sweep pass (temporal blocking above) as a WAVE-PRIVATE march.
 //
 // One workgroup = one wave of 64 lanes; lane l owns the column pair
 // (c0, c0+1), c0 = j0 - 2H + 2l.  Everything a stage needs lives in the
@@ -610,7 +610,7 @@ __device__ __forceinline__ void march_units(const MarchRegions &reg, int wpb, lo
 // wave_shl:1).  No LDS and no barriers: the stage chain is a short run of
 // dependent fp64 VALU ops, and the two to three waves per SIMD overlap.
 //
-// Schedule (as k_smooth): at step s stage h (h = 0..S-1, S = 2K) updates
+// Schedule: at step s stage h (h = 0..S-1, S = 2K) updates
 // its colour in row s+1-h; the residual stage (RESTRICT / NORM) takes row
 // s+1-S; row s+2-S is final and stored.  u rows s-S .. s+3 are live (S+4 =
 // NR rows), rhs/v rows s+1-S .. s+WRV (loaded WRV steps ahead, MGX_WRV);
@@ -619,7 +619,7 @@ __device__ __forceinline__ void march_units(const MarchRegions &reg, int wpb, lo
 // constant.
 //
 // The exact cone, halo lanes (H = ceil(E/2) pairs per side), clamped
-// unconditional loads, Markstein division and modes are those of k_smooth;
+// unconditional loads, Markstein division and modes are those above;
 // each exact value is computed from exactly the operands of the sequential
 // gs.cpp sweeps (bitwise).  The velocity terms enter as t = v*(h/2), which
 // is bitwise v*h/2.0 (scaling by 2^-1 is exact for these magnitudes), so a(v)
@@ -1400,13 +1400,13 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
 }
 
 // k_smooth_tile: the same fused pass (K sweeps + optional prolong / restrict
-// / norm) for SMALL levels, where the serial row march of k_smooth is latency
+// / norm) for SMALL levels, where the serial row march is latency
 // bound.  A workgroup owns a TR x TC output tile and loads it with an EH-wide
 // halo (EH = E rounded up to even, so the tile origin has even parity) into
 // LDS; all stages then run as parallel colour updates over the whole
 // extended tile with one barrier between stages.  The exact region shrinks
 // by one point per stage, so the output tile is exact (same argument as
-// k_smooth).  Each lane owns fixed column pairs of the tile and keeps their
+// the row march).  Each lane owns fixed column pairs of the tile and keeps their
 // rhs / v1 / v2 in registers for all stages.
 // threads per tile workgroup: 1024 (2 pairs per thread, ~80-105 VGPRs)
 // against 256 (8 pairs, 155-189 VGPRs): levels 3-7 0.289 -> 0.237 ms per
