@@ -3,7 +3,7 @@ context vs G virtual ranks (mgx_create_local_dist), per-kind device times.
 The virtual ranks run one after another on one stream, so G parts ~ 1 GPU's
 work + the partition overheads (ghost rows recomputed, exchanges, more
 launches, replicated coarse levels G times).
-    python tools/ab_dist.py [--N 16384 --L 9] [--parts 1,2,4,8] [--cycles 5]"""
+    python tools/ab_dist.py [--N 16384 --L 9] [--parts 1,2,4,8] [--cycles 5] [--tower correct]"""
 import argparse, json, sys, time
 sys.path.insert(0, '.')
 import hpcclassmultigridproject_amd as pkg
@@ -16,6 +16,8 @@ ap.add_argument('--cycles', type=int, default=5)
 ap.add_argument('--rounds', type=int, default=2)
 ap.add_argument('--min-rows', default='256')
 ap.add_argument('--overlap', default='0', help='dist_overlap values to compare, e.g. 0,1')
+ap.add_argument('--tower', choices=['reference', 'correct'], default='reference',
+                help='correct: no whole-grid staging buffers (N=65536 on one GPU)')
 a = ap.parse_args()
 N, L = a.N, a.L
 dt = 1.0 / N / 10
@@ -28,8 +30,15 @@ for rnd in range(a.rounds):
     for G in [int(x) for x in a.parts.split(',')]:
         if G == 1 and ov:
             continue
-        mg = pkg.Multigrid(N, L, dt, -4e-4, device=0, local_parts=G if G > 1 else 0)
-        mg.upload(u0, v1, v2); mg.rhs(); mg.run_cycles(1); mg.synchronize()
+        mg = pkg.Multigrid(N, L, dt, -4e-4, device=0, local_parts=G if G > 1 else 0,
+                           tower_mode=_lib.TOWER_CORRECT if a.tower == 'correct'
+                           else _lib.TOWER_REFERENCE)
+        if G > 1 and a.tower == 'correct':   # row-block upload (no whole-grid staging)
+            mg.upload_rows([pkg.init_problem_rows(N, lo, hi + 1, nthreads=16)
+                            for lo, hi in (mg.dist_rows(p) for p in range(G))])
+        else:
+            mg.upload(u0, v1, v2)
+        mg.rhs(); mg.run_cycles(1); mg.synchronize()
         mg.profile_reset(); mg.profile(True)
         t = time.perf_counter(); r = mg.run_cycles(a.cycles); mg.synchronize()
         ms = (time.perf_counter() - t) / a.cycles * 1e3
