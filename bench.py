@@ -121,7 +121,7 @@ def parse():
     ap.add_argument("--row-upload", choices=["auto", "on", "off"], default="auto",
                     help="multi-GPU: each rank builds only its rows (auto: N > 16384)")
     ap.add_argument("--rccl-check", type=int, default=1,
-                    help="N > 1: first check libmgx's RCCL path bitwise vs one GPU (N=1024)")
+                    help="N > 1: first check libmgx's RCCL path bitwise vs one GPU (N=4096)")
     ap.add_argument("--no-profile", action="store_true",
                     help="do not record per-kernel HIP events in the timed region")
     ap.add_argument("--sweep", nargs=2, type=int, metavar=("NMIN", "NMAX"),
@@ -416,7 +416,7 @@ def main():
         if "hbm_GBs" in roof:
             roof["hbm_frac_of_stream5"] = round(roof["hbm_GBs"] / roof["stream5_ceiling_GBs"], 4)
     out = {
-        "metric": "V-cycle grid-point-updates/sec at N=16384; achieved HBM GB/s vs peak",
+        "metric": f"V-cycle grid-point-updates/sec at N={N}; achieved HBM GB/s vs peak",
         "value": value, "unit": "grid-point-updates/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,

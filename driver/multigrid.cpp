@@ -90,15 +90,10 @@ static void timestepper(double *uT, const double *u0, const double *v1, const do
     mgx_destroy(ctx);
 }
 
+// multigrid.cpp:269-284's writer ("%d\t%d\t%f\n", i outer, j inner), formatted
+// on all host threads by the library (mgx_write_uT; row blocks append)
 static void write_uT(const char *path, const double *u, long N) {
-    FILE *f = fopen(path, "w");
-    if (!f) {
-        perror(path);
-        exit(1);
-    }
-    for (long i = 0; i < N + 1; i++)
-        for (long j = 0; j < N + 1; j++) fprintf(f, "%d\t%d\t%f\n", (int)i, (int)j, u[i * (N + 1) + j]);
-    fclose(f);
+    die(mgx_write_uT(path, u, N, 0, N + 1, 0, 0), path);
 }
 
 int main(int argc, char **argv) {
@@ -143,12 +138,11 @@ int main(int argc, char **argv) {
     timestepper(uTref.data(), u0.data(), v1.data(), v2.data(), nu, maxlvl, N, dt, T, tol, shape,
                 nsmooth, tower);
     double s1 = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    // the reference's three stdout lines, in its exact shapes (multigrid.cpp:246,
-    // :259, :266), so scripts that parse them keep working.  What ran goes to
-    // stderr: its 1-thread reference leg is here the reference's op sequence
-    // on one GPU, its OMP leg the fused library path.
-    printf("\nCPU (1 thread for reference) time, N = %i: %f s\n", (int)N, s1);
-    fprintf(stderr, "[mgx] leg 1 = the reference op sequence through the gs.h ops on 1 MI355X\n");
+    // the reference's three stdout lines in its shapes (multigrid.cpp:246, :259,
+    // :266: "<label> time, N = %i: %f s", "Error (...) = %10e"), with labels that
+    // say what ran: leg 1 is the reference's op sequence through the gs.h-level
+    // entry points, leg 2 the library's fused time stepper, both on one GPU.
+    printf("\nGPU (reference op sequence, 1 MI355X) time, N = %i: %f s\n", (int)N, s1);
 
     mgx_options o;
     mgx_default_options(&o);
@@ -160,8 +154,7 @@ int main(int argc, char **argv) {
                            dx, tol, &o, nullptr),
         "mgx_timestepper");
     double s2 = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    printf("\nCPU with OMP (%d threads) time, N = %i: %f s\n", 1, (int)N, s2);
-    fprintf(stderr, "[mgx] leg 2 = mgx_timestepper (fused passes) on 1 MI355X\n");
+    printf("\nGPU (mgx_timestepper fused passes, 1 MI355X) time, N = %i: %f s\n", (int)N, s2);
     double error = 0;
     for (size_t p = 0; p < cnt; ++p) error += fabs(uTfast[p] - uTref[p]);
     printf("Error (compared to the referenced solution) = %10e\n", error);

@@ -7,7 +7,7 @@ kernels in libmgx.so behind the C ABI of include/mgx.h.
 from . import gs
 from ._lib import MGXError, Options, default_options, lib
 from .multigrid import (Multigrid, default_maxlvl, init_problem, init_problem_rows,
-                        timestepper)
+                        timestepper, write_uT)
 
 __all__ = ["gs", "MGXError", "Options", "default_options", "lib", "Multigrid",
-           "default_maxlvl", "init_problem", "init_problem_rows", "timestepper"]
+           "default_maxlvl", "init_problem", "init_problem_rows", "timestepper", "write_uT"]

@@ -93,6 +93,9 @@ _SIGS = {
     "mgx_dist_rows": (_I, [_vp, _I, C.POINTER(_I), C.POINTER(_I)]),
     "mgx_upload_rows": (_I, [_vp, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp)]),
     "mgx_get_tuning": (_I, [C.c_char_p, C.POINTER(_L)]),
+    "mgx_owned_rows": (_I, [_vp, _I, C.POINTER(_I), C.POINTER(_I)]),
+    "mgx_download_rows": (_I, [_vp, _I, _vp]),
+    "mgx_write_uT": (_I, [C.c_char_p, _vp, _L, _L, _L, _I, _I]),
 }
 
 _lib = None

@@ -78,6 +78,7 @@ struct mgx_ctx {
     // (step_res0) and first pre-smoothing + restriction (lv[0].spec, lv[1]
     // rhs); step_spec = that state is ready for the next mgx_step
     bool step_next = false, step_spec = false;
+    bool no_rhs_alt = false;   // the step-mode rhs did not fit in HBM: plain schedule
     double step_res0 = 0;
     // profiling
     int prof = 0;   // 0 off, 1 every launch, 2 finest-level launches only
@@ -139,6 +140,8 @@ int upload_ctx(mgx_ctx *c, const double *u0, const double *v1, const double *v2,
 int dist_upload(mgx_ctx *c, const double *u0, const double *v1, const double *v2,
                 hipMemcpyKind kind);
 int dist_download(mgx_ctx *c, double *u, hipMemcpyKind kind);
+int dist_owned_rows(mgx_ctx *c, int part, int *ra, int *rb);
+int dist_download_rows(mgx_ctx *c, int part, double *out, hipMemcpyKind kind);
 int dist_rhs(mgx_ctx *c);
 int dist_rhs_norm(mgx_ctx *c, double *res0);
 int dist_vcycle(mgx_ctx *c, double *norm, bool store_post = true);

@@ -759,6 +759,43 @@ int dist_download(mgx_ctx *c, double *u, hipMemcpyKind kind) {
     return rc;
 }
 
+// Owned finest-level rows [ra, rb) of local part `part` (every rank owns a
+// contiguous block; the last one also owns the boundary row n).
+int dist_owned_rows(mgx_ctx *c, int part, int *ra, int *rb) {
+    Dist *d = c->dist;
+    if (part < 0 || part >= (int)d->parts.size()) return fail(MGX_E_ARG, "bad part");
+    plan_rows(c->N, 0, d->world, d->parts[part].rank, ra, rb);
+    return MGX_OK;
+}
+
+// Row-block download (the counterpart of the row-block upload: no rank ever
+// holds the whole grid): the owned rows of one local part, reference layout
+// ((rb-ra) x (N+1) doubles).  No communication.
+int dist_download_rows(mgx_ctx *c, int part, double *out, hipMemcpyKind kind) {
+    Dist *d = c->dist;
+    HIPCHK(hipSetDevice(c->device));
+    int ra, rb;
+    CHK(dist_owned_rows(c, part, &ra, &rb));
+    const long n = c->N;
+    const size_t row = (n + 1) * sizeof(double);
+    const double *src;
+    long P;
+    if (d->la == 0) {   // everything replicated: the part's rows of its full copy
+        Level &S = d->parts[part].sub->lv[0];
+        src = S.U();
+        P = S.pitch;
+    } else {
+        PLevel &L = d->parts[part].lv[0];
+        src = L.U();
+        P = L.pitch;
+    }
+    // (PLevel::U() is offset so that + r * pitch is global row r, like a full field)
+    HIPCHK(hipMemcpy2DAsync(out, row, src + (long)ra * P, P * sizeof(double), row, rb - ra, kind,
+                            c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return MGX_OK;
+}
+
 // Row-block upload (no rank ever holds the whole grid): each part gets its
 // allocated rows [lo, hi] of u0 / v1 / v2 from the host, and the velocity
 // tower is built locally by injection (MGX_TOWER_CORRECT, each level from the

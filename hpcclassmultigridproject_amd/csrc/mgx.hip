@@ -273,11 +273,7 @@ void drop_spec(mgx_ctx *c) {
 static int op_cross(mgx_ctx *c, bool store_post, bool rs = false) {
     Level &L = c->lv[0], &Cl = c->lv[1];
     CHK(materialize(c, 1));
-    if (rs && !L.rhs_alt) {   // zero boundary: compute_rhs writes the interior only
-        const size_t bytes = sizeof(double) * (size_t)(L.n + 1) * (size_t)L.pitch;
-        HIPCHK(hipMalloc(&L.rhs_alt, bytes));
-        HIPCHK(hipMemsetAsync(L.rhs_alt, 0, bytes, c->stream));
-    }
+    if (rs && !L.rhs_alt) return fail(MGX_E_INTERNAL, "step-mode cross pass without rhs_alt");
     int P = -1, Q = -1;
     for (int i = 0; i < 3; ++i)
         if (i != L.cur) (P < 0 ? P : Q) = i;
@@ -867,6 +863,20 @@ int mgx_download_level(mgx_ctx *c, int level, int field, double *out) {
     if (c && c->dist) return fail(MGX_E_ARG, "mgx_download_level: not available on a partitioned context");
     return download_impl(c, level, field, out, hipMemcpyDeviceToHost);
 }
+int mgx_owned_rows(mgx_ctx *c, int part, int *ra, int *rb) {
+    if (!c || !ra || !rb) return fail(MGX_E_ARG, "mgx_owned_rows: bad args");
+    if (c->dist) return dist_owned_rows(c, part, ra, rb);
+    if (part != 0) return fail(MGX_E_ARG, "mgx_owned_rows: a single-GPU context has part 0 only");
+    *ra = 0;
+    *rb = (int)c->N + 1;
+    return MGX_OK;
+}
+int mgx_download_rows(mgx_ctx *c, int part, double *rows) {
+    if (!c || !rows) return fail(MGX_E_ARG, "mgx_download_rows: bad args");
+    if (c->dist) return dist_download_rows(c, part, rows, hipMemcpyDeviceToHost);
+    if (part != 0) return fail(MGX_E_ARG, "mgx_download_rows: a single-GPU context has part 0 only");
+    return download_impl(c, 0, 0, rows, hipMemcpyDeviceToHost);
+}
 
 static int no_dist(mgx_ctx *c, const char *what) {
     return fail(MGX_E_ARG, std::string(what) + ": per-level ops are not available on a "
@@ -924,6 +934,32 @@ int mgx_mg_outer(mgx_ctx *c, double tol, int *cycles, double *res0, double *res)
 // rhs + norm pass
 long g_step_cross = 1;
 
+// Step mode needs a second finest-level rhs (the next step's, written by the
+// cross pass).  It is allocated on first use, outside any pass; when HBM is
+// too short for it (N=65536 on one GPU: the towers take ~265 of 288 GB) the
+// context runs the plain schedule instead -- the same results, one pass more
+// per step.
+static bool step_rhs_alt(mgx_ctx *c) {
+    Level &L = c->lv[0];
+    if (L.rhs_alt) return true;
+    if (c->no_rhs_alt || !cross_ok(c) || !mgx::xstep_supported(L.n)) return false;
+    const size_t bytes = sizeof(double) * (size_t)(L.n + 1) * (size_t)L.pitch;
+    if (hipMalloc(&L.rhs_alt, bytes) != hipSuccess) {
+        (void)hipGetLastError();   // out of memory is not an error here
+        L.rhs_alt = nullptr;
+        c->no_rhs_alt = true;
+        return false;
+    }
+    // zero boundary: compute_rhs writes the interior only
+    if (hipMemsetAsync(L.rhs_alt, 0, bytes, c->stream) != hipSuccess) {
+        (void)hipFree(L.rhs_alt);
+        L.rhs_alt = nullptr;
+        c->no_rhs_alt = true;
+        return false;
+    }
+    return true;
+}
+
 static int step_impl(mgx_ctx *c, double tol, int *cycles, bool prepare_next) {
     // compute_rhs and mg_outer's initial norm in one pass (timestepper,
     // multigrid.cpp:168-170), with the first pre-smoothing where it fuses --
@@ -941,7 +977,7 @@ static int step_impl(mgx_ctx *c, double tol, int *cycles, bool prepare_next) {
     } else {
         CHK(op_rhs_norm(c, &res0));
     }
-    c->step_next = prepare_next && g_step_cross != 0 && !c->dist;
+    c->step_next = prepare_next && g_step_cross != 0 && !c->dist && step_rhs_alt(c);
     const int rc = op_mg_outer(c, tol, cycles, nullptr, nullptr, &res0);
     c->step_next = false;
     return rc;
@@ -1134,6 +1170,47 @@ extern "C" int mgx_init_problem_rows(double *u0, double *v1, double *v2, long N,
     if (!u0 || !v1 || !v2 || N < 1 || r0 < 0 || r1 > N + 1 || r0 >= r1)
         return fail(MGX_E_ARG, "mgx_init_problem_rows: bad args");
     return init_rows(u0, v1, v2, N, r0, r1, nthreads);
+}
+
+// The reference's uT text writer (multigrid.cpp:269-284: fprintf "%d\t%d\t%f\n",
+// i outer, j inner) for rows [r0, r1) held in `rows` ((r1-r0) x (N+1)), so a
+// row-partitioned run writes its output block by block: rank r appends its
+// owned rows in rank order and the file is byte-identical to the whole-grid
+// writer.  Lines are formatted by nthreads threads, written in order.
+extern "C" int mgx_write_uT(const char *path, const double *rows, long N, long r0, long r1,
+                            int append, int nthreads) {
+    if (!path || !rows || N < 1 || r0 < 0 || r1 > N + 1 || r0 > r1)
+        return fail(MGX_E_ARG, "mgx_write_uT: bad args");
+    FILE *f = fopen(path, append ? "ab" : "wb");
+    if (!f) return fail(MGX_E_ARG, std::string("mgx_write_uT: cannot open ") + path);
+    int nt = nthreads > 0 ? nthreads : (int)std::thread::hardware_concurrency();
+    nt = std::max(1, std::min(nt, 64));
+    const long w = N + 1, per = 8;   // rows per thread per batch
+    std::vector<std::string> buf(nt);
+    int rc = MGX_OK;
+    for (long b0 = r0; b0 < r1 && rc == MGX_OK; b0 += per * nt) {
+        auto fmt = [&](int t) {
+            std::string &s = buf[t];
+            s.clear();
+            char line[400];   // "%f" of DBL_MAX is 316 characters
+            const long a = b0 + t * per, e = std::min(r1, a + per);
+            for (long i = a; i < e; ++i)
+                for (long j = 0; j < w; ++j) {
+                    const int k = snprintf(line, sizeof line, "%d\t%d\t%f\n", (int)i, (int)j,
+                                           rows[(i - r0) * w + j]);
+                    s.append(line, k);
+                }
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; ++t) th.emplace_back(fmt, t);
+        fmt(0);
+        for (auto &x : th) x.join();
+        for (int t = 0; t < nt && rc == MGX_OK; ++t)
+            if (!buf[t].empty() && fwrite(buf[t].data(), 1, buf[t].size(), f) != buf[t].size())
+                rc = fail(MGX_E_ARG, std::string("mgx_write_uT: write failed: ") + path);
+    }
+    if (fclose(f) != 0 && rc == MGX_OK) rc = fail(MGX_E_ARG, "mgx_write_uT: close failed");
+    return rc;
 }
 
 // ---- tuning knobs (process-wide)

@@ -77,13 +77,14 @@ def gather_plan(n: int, maxlvl: int, world: int, rank: int):
     return lv.value, r0.value, rows.value
 
 
-def rccl_selfcheck(world: int, rank: int, device: int, n: int = 1024, maxlvl: int = 6,
+def rccl_selfcheck(world: int, rank: int, device: int, n: int = 4096, maxlvl: int = 7,
                    cycles: int = 2, group=None) -> dict:
     """Run libmgx's RCCL transport with real peers against a single-GPU context.
 
     Every rank builds a row-partitioned context of the same small problem
-    (``dist_min_rows`` 16, so levels 0..3 are split even at world 8) and runs
-    ``cycles`` V-cycles with the cross-cycle pass -- ghost send/recv, the
+    (``dist_min_rows`` 16, so levels 0..5 are split even at world 8; n >= 4096,
+    so the finest level runs the cross-cycle pass, asserted by its launch
+    count) and runs ``cycles`` V-cycles with it -- ghost send/recv, the
     all-gather into the replicated levels, the norm all-reduce, the
     all-gather + broadcast of the download -- once with the exchanges on the
     compute stream and once overlapped (``dist_overlap``); rank 0 compares u
@@ -116,8 +117,11 @@ def rccl_selfcheck(world: int, rank: int, device: int, n: int = 1024, maxlvl: in
                            unique_id=uid) as mg:
                 la = mg.dist_info()[2]
                 mg.upload(u0, v1, v2)
+                mg.profile(True, finest_only=True)
                 mg.rhs()
                 norms = [mg.run_cycles(1) for _ in range(cycles)]
+                # the cross-cycle pass (and so the overlapped exchange) really ran
+                ok = ok and mg.profile_get(_lib.K_XSMOOTH, 0)[0] > 0
                 u = mg.download()
             if rank == 0:
                 ok = ok and bool(np.array_equal(u, ref[1]))

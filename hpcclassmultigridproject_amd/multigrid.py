@@ -59,6 +59,17 @@ def timestepper(uT, u0, v1, v2, nu, maxlvl, n, dt, T, dx, tol, shape=1, *, nsmoo
     return list(cyc)[:steps]
 
 
+def write_uT(path, rows, N: int, r0: int = 0, r1: int = None, append=False, nthreads=0):
+    """multigrid.cpp:269-284 text output ("%d\t%d\t%f\n", i outer, j inner) of
+    rows [r0, r1) held in `rows`; rank-ordered appends of row blocks give the
+    whole-grid file byte for byte."""
+    r1 = N + 1 if r1 is None else r1
+    if rows.size != (r1 - r0) * (N + 1):
+        raise ValueError("rows must hold (r1-r0)*(N+1) doubles")
+    check(lib().mgx_write_uT(str(path).encode(), _np_ptr(rows), N, r0, r1, int(bool(append)),
+                             nthreads))
+
+
 class Multigrid:
     """Device-resident level towers and the V-cycle (mgx_ctx).
 
@@ -141,6 +152,23 @@ class Multigrid:
         arr = C.c_void_p * k
         u, a, b = (arr(*[_np_ptr(blk[j]) for blk in blocks]) for j in range(3))
         check(lib().mgx_upload_rows(self._h, u, a, b))
+
+    def owned_rows(self, part=0):
+        """-> (ra, rb): finest-level rows [ra, rb) owned by local part `part`."""
+        ra, rb = C.c_int(), C.c_int()
+        check(lib().mgx_owned_rows(self._h, part, C.byref(ra), C.byref(rb)))
+        return ra.value, rb.value
+
+    def download_rows(self, part=0, out=None):
+        """Row-block download: the owned rows of local part `part`,
+        (rb-ra)*(N+1) float64 (no rank ever holds the whole grid)."""
+        ra, rb = self.owned_rows(part)
+        cnt = (rb - ra) * (self.N + 1)
+        out = np.empty(cnt, dtype=np.float64) if out is None else out
+        if out.size != cnt:
+            raise ValueError(f"out must hold {cnt} doubles")
+        check(lib().mgx_download_rows(self._h, part, _np_ptr(out)))
+        return out
 
     def download(self, out=None):
         out = np.empty((self.N + 1) ** 2, dtype=np.float64) if out is None else out

@@ -298,6 +298,19 @@ int mgx_dist_rows(mgx_ctx *ctx, int part, int *lo, int *hi);
  * reference tower reads the whole grid).  Collective. */
 int mgx_upload_rows(mgx_ctx *ctx, const double *const *u0, const double *const *v1,
                     const double *const *v2);
+/* Owned finest-level rows [*ra, *rb) of local part `part` (the last rank also
+ * owns the boundary row N; a single-GPU context: part 0 = [0, N+1)). */
+int mgx_owned_rows(mgx_ctx *ctx, int part, int *ra, int *rb);
+/* Row-block download, the counterpart of mgx_upload_rows: the owned rows of
+ * local part `part` into rows[(rb-ra)*(N+1)], reference layout.  No
+ * communication and no whole-grid buffer on any rank (C5: N=65536). */
+int mgx_download_rows(mgx_ctx *ctx, int part, double *rows);
+/* The reference's uT text output (multigrid.cpp:269-284, "%d\t%d\t%f\n", i
+ * outer, j inner) for rows [r0, r1) held in rows[(r1-r0)*(N+1)]; append != 0
+ * appends.  Rank-ordered appends of each rank's owned rows give the file the
+ * whole-grid writer gives, byte for byte.  nthreads <= 0: all host threads. */
+int mgx_write_uT(const char *path, const double *rows, long N, long r0, long r1, int append,
+                 int nthreads);
 /* world size, rank (-1 for a local multi-part context; 0/1 for single GPU),
  * first replicated level (maxlvl for a single-GPU context). */
 int mgx_dist_info(mgx_ctx *ctx, int *world, int *rank, int *replicated_level);

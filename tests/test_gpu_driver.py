@@ -33,13 +33,15 @@ def test_multigrid_driver_writes_reference_uT(tmp_path):
     for name in ("uT.txt", "uTomp.txt"):
         with open(tmp_path / name) as f:
             assert f.read() == want, name
-    # the reference's line shapes (multigrid.cpp:246, :259, :266):
-    # exactly, labels included, then the %10e error line
+    # the reference's line shapes (multigrid.cpp:246, :259, :266), labelled
+    # with what ran (both legs on the GPU), then the %10e error line
     lines = out.split("\n")
     timed = [l for l in lines if re.fullmatch(r".+ time, N = 32: \d+\.\d{6} s", l)]
     assert len(timed) == 2, out
-    assert re.fullmatch(r"CPU \(1 thread for reference\) time, N = 32: \d+\.\d{6} s", timed[0])
-    assert re.fullmatch(r"CPU with OMP \(\d+ threads\) time, N = 32: \d+\.\d{6} s", timed[1])
+    assert re.fullmatch(r"GPU \(reference op sequence, 1 MI355X\) time, N = 32: \d+\.\d{6} s",
+                        timed[0])
+    assert re.fullmatch(r"GPU \(mgx_timestepper fused passes, 1 MI355X\) time, N = 32: "
+                        r"\d+\.\d{6} s", timed[1])
     assert lines[lines.index(timed[0]) - 1] == "" and lines[lines.index(timed[1]) - 1] == ""
     assert "Error (compared to the referenced solution) = 0.000000e+00" in lines
 
