@@ -54,7 +54,8 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s HBM3E
 # PMC traffic summary committed under profiles/ (tools/profile_round.sh)
 # (the cross pass is two launches: the unguarded interior kernel and the
 # guarded edge kernel; their traffic is summed)
-KERNEL_IDS = {(8, 0): ("mgx::k_xsmooth<4, 3, false, false>", "mgx::k_xsmooth<1, 3, true, false>"),
+KERNEL_IDS = {(8, 0): ("mgx::k_xsmooth<4, 3, false, false, true>",
+                       "mgx::k_xsmooth<1, 3, true, false, true>"),
               (0, 0): ("mgx::k_wsmooth<4, 3, 4, true>",),
               (7, 0): ("mgx::k_wsmooth<4, 3, 10, true>",)}
 KERNELS_HIP = os.path.join(ROOT, "hpcclassmultigridproject_amd", "csrc", "kernels.hip")

@@ -96,6 +96,8 @@ _SIGS = {
     "mgx_owned_rows": (_I, [_vp, _I, C.POINTER(_I), C.POINTER(_I)]),
     "mgx_download_rows": (_I, [_vp, _I, _vp]),
     "mgx_write_uT": (_I, [C.c_char_p, _vp, _L, _L, _L, _I, _I]),
+    "mgx_factor_velocity": (_I, [_vp, _L, _L, _D, _vp, _vp]),
+    "mgx_velocity_factored": (_I, [_vp, C.POINTER(_I)]),
 }
 
 _lib = None

@@ -40,6 +40,10 @@ struct Level {
     int nxt() const { return cur == 0 ? 1 : 0; }   // ping-pong partner of cur
     double *rhs = nullptr, *v1 = nullptr, *v2 = nullptr;
     double *rhs_alt = nullptr;   // finest level: the next time step's rhs (step mode)
+    // exact rank-1 factors of v1 / v2 (sepvel.h; row factors n+1, column
+    // factors pitch, zero padded), or null: the passes that take them read
+    // the 2-D v1 / v2 from HBM only where no factors exist
+    double *sa1 = nullptr, *sb1 = nullptr, *sa2 = nullptr, *sb2 = nullptr;
     mgx::Coef coef{};
     double M() const { return double(n + 1) * double(n + 1); }
     double *U() const { return u[cur]; }
@@ -129,6 +133,16 @@ int op_vcycle(mgx_ctx *c, int l, double *norm = nullptr, bool store_post = true)
 int op_rhs(mgx_ctx *c);
 int op_residual_norm(mgx_ctx *c, int l, double *norm, double bytes_per_pt = 48.0);
 int build_tower(mgx_ctx *c);
+// velocity factors of level 0 from host copies of v1 / v2 (rows [r0, r0+rows)
+// of width n+1); false: not separable (or "sep_velocity" off), nothing set
+bool factor_velocity(const double *v1, const double *v2, long n, long r0, long rows, double smin,
+                     std::vector<double> &a1, std::vector<double> &b1, std::vector<double> &a2,
+                     std::vector<double> &b2);
+int set_level_factors(Level &L, long row0, const std::vector<double> &a1,
+                      const std::vector<double> &b1, const std::vector<double> &a2,
+                      const std::vector<double> &b2, hipStream_t s);
+void free_level_factors(Level &L);
+extern long g_sep_velocity;
 void free_ctx(mgx_ctx *c);
 // Create a single-GPU context; stream != nullptr: borrow that stream.
 int create_ctx(mgx_ctx **out, long n, int maxlvl, double dt, double nu, const mgx_options *opt,

@@ -74,6 +74,9 @@ struct PLevel {
     int xin = -1;    // level 0: input buffer of the last cross-cycle pass (Level::xin)
     bool zero = false;
     double *rhs = nullptr, *v1 = nullptr, *v2 = nullptr;
+    // level 0: exact velocity factors (sepvel.h) indexed by GLOBAL row / column
+    // (full-length arrays, this block's rows filled), or null
+    double *sa1 = nullptr, *sb1 = nullptr, *sa2 = nullptr, *sb2 = nullptr;
     mgx::Coef coef{};
     int nxt() const { return cur == 0 ? 1 : 0; }
     // field pointer offset so that F(a) + r*pitch is global row r
@@ -113,6 +116,7 @@ void dist_free(mgx_ctx *c) {
             (void)hipFree(L.rhs);
             (void)hipFree(L.v1);
             (void)hipFree(L.v2);
+            for (double *f : {L.sa1, L.sb1, L.sa2, L.sb2}) (void)hipFree(f);
         }
         if (p.sub) free_ctx(p.sub);
         (void)hipFree(p.dsum);
@@ -228,11 +232,9 @@ static int exchange_rows(mgx_ctx *c, std::initializer_list<XF> xs, hipStream_t s
     return MGX_OK;
 }
 
-static int exchange(mgx_ctx *c, std::initializer_list<XF> xs) {
-    if (c->dist->world == 1 || xs.size() == 0) return MGX_OK;
-    int rc = MGX_OK;
-    // bytes moved by the parts this process holds: every row sent is read once
-    // and written once
+// bytes moved by the parts this process holds: every row sent is read once
+// and written once
+static double halo_bytes(mgx_ctx *c, std::initializer_list<XF> xs) {
     double bytes = 0;
     std::vector<Xfer> plan;
     for (const XF &x : xs)
@@ -240,7 +242,13 @@ static int exchange(mgx_ctx *c, std::initializer_list<XF> xs) {
             ghost_plan(c->N, x.l, c->dist->world, p.rank, plan);
             for (const Xfer &t : plan) bytes += 16.0 * t.send_rows * p.lv[x.l].pitch;
         }
-    CHK(launch(c, MGX_K_HALO, xs.begin()->l, bytes,
+    return bytes;
+}
+
+static int exchange(mgx_ctx *c, std::initializer_list<XF> xs) {
+    if (c->dist->world == 1 || xs.size() == 0) return MGX_OK;
+    int rc = MGX_OK;
+    CHK(launch(c, MGX_K_HALO, xs.begin()->l, halo_bytes(c, xs),
                [&] { rc = exchange_rows(c, xs, c->stream); }));
     return rc;
 }
@@ -444,7 +452,16 @@ static int dist_cross(mgx_ctx *c, bool store_post) {
     if (ov) {
         HIPCHK(hipEventRecord(d->ev_fork, c->stream));
         HIPCHK(hipStreamWaitEvent(d->xs, d->ev_fork, 0));
+        // profiled like a launch, on the side stream (launch() times c->stream)
+        const bool rec = c->prof == 1 || c->prof == 2;
+        hipEvent_t e0 = rec ? take_event(c) : nullptr, e1 = rec ? take_event(c) : nullptr;
+        if (e0) HIPCHK(hipEventRecord(e0, d->xs));
         CHK(exchange_rows(c, 1 < d->la ? xs : x0, d->xs));
+        if (e0 && e1) {
+            HIPCHK(hipEventRecord(e1, d->xs));
+            const double b = halo_bytes(c, 1 < d->la ? xs : x0);
+            c->pending.push_back({MGX_K_HALO, 0, b, b, e0, e1});
+        }
         HIPCHK(hipEventRecord(d->ev_join, d->xs));
     } else {
         CHK(exchange(c, 1 < d->la ? xs : x0));
@@ -481,13 +498,18 @@ static int dist_cross(mgx_ctx *c, bool store_post) {
         A.pitch = L.pitch;
         A.c = L.coef;
         A.store_post = store_post;
+        A.sa1 = L.sa1;
+        A.sb1 = L.sb1;
+        A.sa2 = L.sa2;
+        A.sb2 = L.sb2;
         A.ra = ra;
         A.rb = rb;
         A.lo = L.lo;
         A.hi = L.hi;
         if (rb - ra < 4 * G) A.min_rows = 8;   // a band: many short segments
         const double bytes = (32.0 + 40.0 * k + 48.0 + 40.0 * k + 40.0) * Mown + 32.0 * Mc;
-        const double cbytes = 8.0 * ((store_post ? 6.0 : 5.0) * Mown + 2.0 * Mc);
+        const double cbytes =
+            8.0 * ((store_post ? 6.0 : 5.0) * Mown - (L.sa1 ? 2.0 * Mown : 0.0) + 2.0 * Mc);
         int blocks = 0;
         CHK(launch(c, MGX_K_XSMOOTH, 0, bytes, cbytes,
                    [&] { blocks = mgx::launch_xsmooth(A, k, c->stream); }));
@@ -655,6 +677,36 @@ mgx_ctx *dist_sub(mgx_ctx *c, int i) { return c->dist->parts[i].sub; }
 int dist_la(mgx_ctx *c) { return c->dist ? c->dist->la : c->L; }
 
 // ---------------------------------------------------------------- data movement
+// Level-0 velocity factors of a part: device copies of full-length arrays
+// (row factors n+1, column factors pitch), from device (T's) or host vectors
+// covering rows [row0, row0 + rows).
+static void drop_factors(PLevel &L) {
+    for (double **f : {&L.sa1, &L.sb1, &L.sa2, &L.sb2}) {
+        (void)hipFree(*f);
+        *f = nullptr;
+    }
+}
+static int part_factors(PLevel &L, const double *a1, const double *b1, const double *a2,
+                        const double *b2, long row0, long rows, hipMemcpyKind kind,
+                        hipStream_t st) {
+    drop_factors(L);
+    const size_t ra = sizeof(double) * (size_t)(L.n + 1), rb = sizeof(double) * (size_t)L.pitch;
+    HIPCHK(hipMalloc(&L.sa1, ra));
+    HIPCHK(hipMalloc(&L.sa2, ra));
+    HIPCHK(hipMalloc(&L.sb1, rb));
+    HIPCHK(hipMalloc(&L.sb2, rb));
+    for (double *f : {L.sa1, L.sa2}) HIPCHK(hipMemsetAsync(f, 0, ra, st));
+    for (double *f : {L.sb1, L.sb2}) HIPCHK(hipMemsetAsync(f, 0, rb, st));
+    const size_t na = sizeof(double) * (size_t)rows;
+    const size_t nb = sizeof(double) * (size_t)(kind == hipMemcpyHostToDevice ? L.n + 1 : L.pitch);
+    HIPCHK(hipMemcpyAsync(L.sa1 + row0, a1 + (kind == hipMemcpyHostToDevice ? 0 : row0), na, kind, st));
+    HIPCHK(hipMemcpyAsync(L.sa2 + row0, a2 + (kind == hipMemcpyHostToDevice ? 0 : row0), na, kind, st));
+    HIPCHK(hipMemcpyAsync(L.sb1, b1, nb, kind, st));
+    HIPCHK(hipMemcpyAsync(L.sb2, b2, nb, kind, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return MGX_OK;
+}
+
 // Build the full tower in a temporary single-GPU context (the reference
 // construction, multigrid.cpp:148-160), then copy every rank's rows out of it.
 int dist_upload(mgx_ctx *c, const double *u0, const double *v1, const double *v2,
@@ -683,6 +735,13 @@ int dist_upload(mgx_ctx *c, const double *u0, const double *v1, const double *v2
             L.cur = 0;
             L.spec = -1;
             L.zero = false;
+            if (rc == MGX_OK && l == 0) {   // the whole level's velocity factors, if any
+                if (F.sa1)
+                    rc = part_factors(L, F.sa1, F.sb1, F.sa2, F.sb2, 0, L.n + 1,
+                                      hipMemcpyDeviceToDevice, c->stream);
+                else
+                    drop_factors(L);
+            }
         }
         for (int l = d->la; rc == MGX_OK && l < c->L; ++l) {
             Level &S = p.sub->lv[l - d->la];
@@ -826,6 +885,16 @@ static int dist_upload_rows_impl(mgx_ctx *c, const double *const *u0s,
         }
         PLevel &L = p.lv[0];
         const size_t row = w * sizeof(double), rows = L.hi - L.lo + 1;
+        // velocity factors of this block's rows (every rank decides for its own
+        // block: the factors only have to reproduce the rows its passes read)
+        std::vector<double> a1, b1, a2, b2;
+        if (L.n >= kCrossMinN && c->L > 1 &&
+            factor_velocity(v1s[i], v2s[i], c->N, L.lo, (long)rows, L.coef.h * 0.5, a1, b1, a2,
+                            b2))
+            CHK(part_factors(L, a1.data(), b1.data(), a2.data(), b2.data(), L.lo, (long)rows,
+                             hipMemcpyHostToDevice, c->stream));
+        else
+            drop_factors(L);
         HIPCHK(hipMemcpy2DAsync(L.u[0], L.pitch * sizeof(double), u0s[i], row, row, rows,
                                 hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipMemcpy2DAsync(L.v1, L.pitch * sizeof(double), v1s[i], row, row, rows,

@@ -115,6 +115,10 @@ struct XArgs {
     // step's, with its rhs formed from u_post into rhs_next and its initial
     // norm into *norm2_out; partials needs 2 * norm_partials_size() doubles
     double *rhs_next = nullptr, *norm2_out = nullptr;
+    // separable velocity (sepvel.h): v1[R][c] = sa1[R] * sb1[c] exactly (global
+    // row R, column c; sb zero-padded to the pitch), v2 likewise; all four set
+    // = the pass reads rhs and u only (the 2-D v1 / v2 are not touched)
+    const double *sa1 = nullptr, *sb1 = nullptr, *sa2 = nullptr, *sb2 = nullptr;
 };
 int launch_xsmooth(const XArgs &a, int sweeps, hipStream_t s);
 // whether launch_xsmooth supports rhs_next on a whole level of size n

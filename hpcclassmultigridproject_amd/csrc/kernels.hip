@@ -1025,14 +1025,24 @@ struct XCfg {
 // multigrid.cpp:104) into partials2, and smooths and restricts with it --
 // the rhs + norm pass of the next step and this step's post-smoothing pass
 // in one HBM pass.  (B's half of the u_post norm still uses this step's rhs.)
-template <int WPB, int K, bool G, bool RS = false>
+//
+// SV = true (separable velocity, sepvel.h): v1[R][c] = fl(sa1[R] * sb1[c]) and
+// v2 likewise, exactly.  A then reads only rhs and u from HBM: per row it
+// loads the two row factors with scalar loads into an SGPR ring (XRV steps
+// ahead, like the rhs row) and forms t = v*h/2 at the row's first stage as
+// fl(sa[R] * fl(sb[c]*h/2)) -- bitwise fl(v*h/2), the scalings by h/2 being
+// exact (sepvel.h checks the range) -- from the lane's column factors, held
+// in registers for the whole march.
+template <int WPB, int K, bool G, bool RS = false, bool SV = false>
 __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     const double *__restrict__ uin, double *__restrict__ upost, double *__restrict__ upre,
     const double *__restrict__ rhs, const double *__restrict__ v1, const double *__restrict__ v2,
     const double *__restrict__ uc, long pitchc, double *__restrict__ rhsc,
     double *__restrict__ partials, int n, long pitch, MarchRegions reg, long units_per_wg, Coef c,
     int lo, int hi, int store_post, double *__restrict__ rhs_next,
-    double *__restrict__ partials2) {
+    double *__restrict__ partials2, const double *__restrict__ sa1,
+    const double *__restrict__ sb1, const double *__restrict__ sa2,
+    const double *__restrict__ sb2) {
     using X = XCfg<K>;
     constexpr int S = X::S, H = X::H, NR = X::NR, W = X::W, D = X::D, NU = X::NU,
                   NRD = X::NRD, EA = X::EA, EB = X::EB;
@@ -1078,6 +1088,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             double2 X;
             double q00, q01, q10, q11;
         };
+        RowData rd[NR];   // rhs / t1 / t2 rows (ring by row)
         // u rows + coarse parents in flight, a ring by row like rd
         UPre up[NR];
 #pragma unroll
@@ -1113,12 +1124,36 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             v.y = on ? v.y + pv.y : v.y;
             return v;
         };
-        auto load_rv = [&](int R, RowData &d) {
-            const long o = (long)min(max(R, lo), hi) * pitch;
+        // SV: the lane's column factors scaled by h/2 (exact), and a ring of
+        // row factors (wave-uniform: SGPRs), slot q = the rd slot of the row
+        double2 bh1 = make_double2(0.0, 0.0), bh2 = bh1;
+        double ar1[NR], ar2[NR];
+        if (SV) {
+            const double2 b1 = ld2(sb1 + cl), b2 = ld2(sb2 + cl);
+            bh1 = make_double2(b1.x * hh, b1.y * hh);
+            bh2 = make_double2(b2.x * hh, b2.y * hh);
+#pragma unroll
+            for (int i = 0; i < NR; ++i) ar1[i] = ar2[i] = 0.0;
+        }
+        auto load_rv = [&](int R, const int q) {
+            const int Rc = min(max(R, lo), hi);
+            const long o = (long)Rc * pitch;
+            RowData &d = rd[q];
             d.r = ld2((rhs + o) + cl);
-            const double2 x = ld2((v1 + o) + cl), y = ld2((v2 + o) + cl);
-            d.x = make_double2(x.x * hh, x.y * hh);
-            d.y = make_double2(y.x * hh, y.y * hh);
+            if (SV) {
+                ar1[q] = sa1[Rc];
+                ar2[q] = sa2[Rc];
+            } else {
+                const double2 x = ld2((v1 + o) + cl), y = ld2((v2 + o) + cl);
+                d.x = make_double2(x.x * hh, x.y * hh);
+                d.y = make_double2(y.x * hh, y.y * hh);
+            }
+        };
+        // SV: t of the row in slot q, at its first stage
+        auto make_t = [&](const int q) {
+            if (!SV) return;
+            rd[q].x = make_double2(ar1[q] * bh1.x, ar1[q] * bh1.y);
+            rd[q].y = make_double2(ar2[q] * bh2.x, ar2[q] * bh2.y);
         };
         // one red-black stage h of the march step at row phase p on row r
         auto stage = [&](double2 *ur, RowData *rd, const int p, const int h, const int r) {
@@ -1158,7 +1193,6 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
         const bool post = store_post != 0;
 
         double2 ur[NR];
-        RowData rd[NR];
 #pragma unroll
         for (int q = 0; q < NR; ++q) {
             ur[q] = make_double2(0.0, 0.0);
@@ -1223,13 +1257,14 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
 #pragma unroll
             for (int d = 3; d < 3 + XU; ++d) load_u(s0 + d, up[d], d & 1);
 #pragma unroll
-            for (int d = 1; d < XRV; ++d) load_rv(s0 + d, rd[d]);
+            for (int d = 1; d < XRV; ++d) load_rv(s0 + d, d);
             for (;;) {
 #pragma unroll
                 for (int p = 0; p < NR; ++p) {   // s == p (mod NR)
                     const int s = s0 + it + (p & 1);
                     ur[(p + 3) % NR] = make_u(s + 3, up[(p + 3) % NR], (p + 3) & 1);
                     load_u(s + 3 + XU, up[(p + 3 + XU) % NR], (p + 3 + XU) & 1);   // XU ahead
+                    make_t((p + 1) % NR);   // row s+1: first used by stage 0 below
 #pragma unroll
                     for (int h = 0; h < S; ++h) stage(ur, rd, p, h, s + 1 - h);
                     // hand-off: rhs/v row s+1 (first used above), final u row s+2-S
@@ -1270,7 +1305,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                             acc += (keep && rin) ? r0 * r0 : 0.0;
                         }
                     }
-                    load_rv(s + XRV, rd[(p + XRV) % NR]);
+                    load_rv(s + XRV, (p + XRV) % NR);
                     if (p & 1) {   // end of a pair (compile-time)
                         __syncthreads();
                         it += 2;
@@ -2345,14 +2380,14 @@ static int smooth_winst(const SmoothArgs &A, hipStream_t s) {
 }
 
 
-template <int WPB, int K, bool G, bool RS = false>
+template <int WPB, int K, bool G, bool RS = false, bool SV = false>
 static int xsmooth_slots() {
     static int slots = 0;   // resident workgroups of this instantiation
     if (!slots) {
         int dev = 0, cus = 0, per = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_xsmooth<WPB, K, G, RS>,
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_xsmooth<WPB, K, G, RS, SV>,
                                                            128 * WPB, 0);
         slots = std::max(1, cus) * std::max(1, per);
     }
@@ -2362,23 +2397,32 @@ static int xsmooth_slots() {
 // One launch over `reg`; min_rows: the fewest rows per workgroup (each
 // workgroup's march pays a warm-up of ~EA + EB + D rows).  Returns the norm
 // partials written (grid * 2 * WPB: one per wave) at `partials`.
-template <int WPB, int K, bool G, bool RS = false>
-static int xsmooth_launch(const XArgs &A, const MarchRegions &reg, double *partials, int lo, int hi,
-                          long min_rows, long max_wgs, hipStream_t s) {
+template <int WPB, int K, bool G, bool RS, bool SV>
+static int xsmooth_launch_sv(const XArgs &A, const MarchRegions &reg, double *partials, int lo,
+                             int hi, long min_rows, long max_wgs, hipStream_t s) {
     const long total = reg.pre[reg.count];
     if (total <= 0) return 0;
     long upw;
     MarchRegions r;
     using X = XCfg<K>;
-    const unsigned grid = plan_march(reg, WPB, xsmooth_slots<WPB, K, G, RS>(), min_rows, max_wgs,
-                                     X::EA + X::EB + X::D + X::NR / 2, upw, r);
+    const unsigned grid = plan_march(reg, WPB, xsmooth_slots<WPB, K, G, RS, SV>(), min_rows,
+                                     max_wgs, X::EA + X::EB + X::D + X::NR / 2, upw, r);
     // RS: the second partials (the next step's initial norm) at the same
     // offsets, kNormBlocks further on
-    MGX_LAUNCH((k_xsmooth<WPB, K, G, RS>), dim3(grid), dim3(128 * WPB), s, A.uin, A.upost,
+    MGX_LAUNCH((k_xsmooth<WPB, K, G, RS, SV>), dim3(grid), dim3(128 * WPB), s, A.uin, A.upost,
                A.upre, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch, r,
                upw, A.c, lo, hi, A.store_post ? 1 : 0, A.rhs_next,
-               RS ? partials + kNormBlocks : (double *)nullptr);
+               RS ? partials + kNormBlocks : (double *)nullptr, A.sa1, A.sb1, A.sa2, A.sb2);
     return (int)grid * 2 * WPB;
+}
+// SV when the level's velocity factors are given (XArgs::sa1)
+template <int WPB, int K, bool G, bool RS = false>
+static int xsmooth_launch(const XArgs &A, const MarchRegions &reg, double *partials, int lo, int hi,
+                          long min_rows, long max_wgs, hipStream_t s) {
+    if (A.sa1 && A.sb1 && A.sa2 && A.sb2)
+        return xsmooth_launch_sv<WPB, K, G, RS, true>(A, reg, partials, lo, hi, min_rows, max_wgs,
+                                                      s);
+    return xsmooth_launch_sv<WPB, K, G, RS, false>(A, reg, partials, lo, hi, min_rows, max_wgs, s);
 }
 
 static void add_tile_region(TileRegions &r, int c0, int c1, int r0, int r1, int TR) {

@@ -17,10 +17,61 @@
 #include <vector>
 
 #include "ctx.h"
+#include "sepvel.h"
 
 namespace mgxi {
 
 thread_local std::string g_err;
+
+// tuning key "sep_velocity": 1 (default) = at upload, a velocity field that is
+// an exact rank-1 outer product (the reference's rotating flow) is also kept
+// as its factors and the finest-level cross pass reads those instead of the
+// 2-D v1 / v2 (sepvel.h; bitwise the same results); 0 = always the 2-D arrays
+long g_sep_velocity = 1;
+
+bool factor_velocity(const double *v1, const double *v2, long n, long r0, long rows, double smin,
+                     std::vector<double> &a1, std::vector<double> &b1, std::vector<double> &a2,
+                     std::vector<double> &b2) {
+    (void)r0;
+    if (!g_sep_velocity || !v1 || !v2 || rows < 1) return false;
+    const long w = n + 1;
+    a1.assign(rows, 0.0);
+    a2.assign(rows, 0.0);
+    b1.assign(w, 0.0);
+    b2.assign(w, 0.0);
+    return mgxsep::factor_rank1(v1, rows, w, w, smin, a1.data(), b1.data()) &&
+           mgxsep::factor_rank1(v2, rows, w, w, smin, a2.data(), b2.data());
+}
+
+void free_level_factors(Level &L) {
+    for (double **p : {&L.sa1, &L.sb1, &L.sa2, &L.sb2}) {
+        (void)hipFree(*p);
+        *p = nullptr;
+    }
+}
+
+// Device copies: row factors at rows [row0, row0 + a.size()) of an (n+1)-row
+// array (the rest zero), column factors zero padded to the pitch.
+int set_level_factors(Level &L, long row0, const std::vector<double> &a1,
+                      const std::vector<double> &b1, const std::vector<double> &a2,
+                      const std::vector<double> &b2, hipStream_t s) {
+    free_level_factors(L);
+    const size_t ra = sizeof(double) * (size_t)(L.n + 1), rb = sizeof(double) * (size_t)L.pitch;
+    HIPCHK(hipMalloc(&L.sa1, ra));
+    HIPCHK(hipMalloc(&L.sa2, ra));
+    HIPCHK(hipMalloc(&L.sb1, rb));
+    HIPCHK(hipMalloc(&L.sb2, rb));
+    for (double *p : {L.sa1, L.sa2}) HIPCHK(hipMemsetAsync(p, 0, ra, s));
+    for (double *p : {L.sb1, L.sb2}) HIPCHK(hipMemsetAsync(p, 0, rb, s));
+    HIPCHK(hipMemcpyAsync(L.sa1 + row0, a1.data(), sizeof(double) * a1.size(),
+                          hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(L.sa2 + row0, a2.data(), sizeof(double) * a2.size(),
+                          hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(L.sb1, b1.data(), sizeof(double) * b1.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(L.sb2, b2.data(), sizeof(double) * b2.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));   // the host vectors may go out of scope
+    return MGX_OK;
+}
 
 // Cross-cycle fusion of the finest level (k_xsmooth) on levels this large
 // (the row-march regime); tuning key "cross_cycle" turns it off.
@@ -293,6 +344,10 @@ static int op_cross(mgx_ctx *c, bool store_post, bool rs = false) {
     A.pitch = L.pitch;
     A.c = L.coef;
     A.store_post = store_post;
+    A.sa1 = L.sa1;
+    A.sb1 = L.sb1;
+    A.sa2 = L.sa2;
+    A.sb2 = L.sb2;
     if (rs) {
         A.rhs_next = L.rhs_alt;
         A.norm2_out = c->dscal + 6;
@@ -306,9 +361,10 @@ static int op_cross(mgx_ctx *c, bool store_post, bool rs = false) {
     // and the coarse rhs written once
     // (step mode: + compute_rhs and the initial residual norm of the next
     // step, and its rhs written)
+    // (with velocity factors v1 / v2 are not read: two fine arrays fewer)
     const double bytes_rs = rs ? (32.0 + 48.0) * L.M() : 0.0;
-    const double cbytes =
-        8.0 * ((store_post ? 6.0 : 5.0) * L.M() + 2.0 * Cl.M() + (rs ? L.M() : 0.0));
+    const double cbytes = 8.0 * ((store_post ? 6.0 : 5.0) * L.M() - (L.sa1 ? 2.0 * L.M() : 0.0) +
+                                 2.0 * Cl.M() + (rs ? L.M() : 0.0));
     int blocks = 0;
     CHK(launch(c, MGX_K_XSMOOTH, 0, bytes + bytes_rs, cbytes,
                [&] { blocks = mgx::launch_xsmooth(A, k, c->stream); }));
@@ -613,6 +669,7 @@ void free_ctx(mgx_ctx *c) {
         (void)hipFree(L.rhs_alt);
         (void)hipFree(L.v1);
         (void)hipFree(L.v2);
+        free_level_factors(L);
     }
     (void)hipFree(c->partials);
     (void)hipFree(c->dscal);
@@ -822,6 +879,13 @@ int mgxi::upload_ctx(mgx_ctx *c, const double *u0, const double *v1, const doubl
         c->lv[l].zero = false;
     }
     CHK(build_tower(c));
+    // exact velocity factors for the finest level's cross pass (host data only;
+    // a device upload keeps the 2-D arrays)
+    free_level_factors(L);
+    std::vector<double> a1, b1, a2, b2;
+    if (kind == hipMemcpyHostToDevice && c->L > 1 && c->N >= kCrossMinN &&
+        factor_velocity(v1, v2, c->N, 0, c->N + 1, L.coef.h * 0.5, a1, b1, a2, b2))
+        CHK(set_level_factors(L, 0, a1, b1, a2, b2, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return MGX_OK;
 }
@@ -1213,6 +1277,22 @@ extern "C" int mgx_write_uT(const char *path, const double *rows, long N, long r
     return rc;
 }
 
+// sepvel.h's exact rank-1 factorisation, for tests: v (rows x (n+1)) ==
+// fl(a[i] * b[j]) bitwise -> 1 (a, b filled), else 0.  Host only.
+extern "C" int mgx_factor_velocity(const double *v, long rows, long n, double smin, double *a,
+                                   double *b) {
+    if (!v || !a || !b || rows < 1 || n < 1) return fail(MGX_E_ARG, "mgx_factor_velocity: bad args");
+    return mgxsep::factor_rank1(v, rows, n + 1, n + 1, smin, a, b) ? 1 : 0;
+}
+
+// whether the context's finest level holds velocity factors (its cross pass
+// reads rhs and u only)
+extern "C" int mgx_velocity_factored(mgx_ctx *c, int *factored) {
+    if (!c || !factored) return fail(MGX_E_ARG, "mgx_velocity_factored: bad args");
+    *factored = (!c->lv.empty() && c->lv[0].sa1) ? 1 : 0;
+    return MGX_OK;
+}
+
 // ---- tuning knobs (process-wide)
 extern "C" int mgx_set_tuning(const char *key, long value) {
     if (!key) return fail(MGX_E_ARG, "mgx_set_tuning: null key");
@@ -1295,6 +1375,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgx::set_coarse_lds(value);
         return MGX_OK;
     }
+    if (!strcmp(key, "sep_velocity")) {
+        if (value != 0 && value != 1) return fail(MGX_E_ARG, "sep_velocity must be 0 or 1");
+        mgxi::g_sep_velocity = value;
+        return MGX_OK;
+    }
     return fail(MGX_E_ARG, std::string("mgx_set_tuning: unknown key ") + key);
 }
 extern "C" int mgx_get_tuning(const char *key, long *value) {
@@ -1362,6 +1447,10 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "coarse_lds")) {
         *value = mgx::get_coarse_lds();
+        return MGX_OK;
+    }
+    if (!strcmp(key, "sep_velocity")) {
+        *value = mgxi::g_sep_velocity;
         return MGX_OK;
     }
     return fail(MGX_E_ARG, std::string("mgx_get_tuning: unknown key ") + key);

@@ -218,6 +218,18 @@ int mgx_synchronize(mgx_ctx *ctx);
  * relative (other reduction trees; a cycle count could differ only on a norm
  * that far from tol). */
 int mgx_set_tuning(const char *key, long value);
+/* "sep_velocity": 1 (default) = a velocity field that is an exact rank-1
+ * outer product in floating point, v[i][j] == a[i]*b[j] bitwise (the
+ * reference's rotating flow, multigrid.cpp:221-222, is one), is detected at
+ * upload and the finest level's cross pass reads its factors instead of the
+ * 2-D v1 / v2 (two of its five input streams); 0 = always the 2-D arrays.
+ * Bitwise the same results either way. */
+/* Host only: exact rank-1 factors of v (rows x (n+1), row-major):
+ * returns 1 and fills a[rows], b[n+1] with fl(a[i]*b[j]) == v[i][j] (same
+ * bits) and every nonzero |v|, |b| still normal after scaling by smin, else 0. */
+int mgx_factor_velocity(const double *v, long rows, long n, double smin, double *a, double *b);
+/* *factored = 1 when the context keeps velocity factors for its finest level. */
+int mgx_velocity_factored(mgx_ctx *ctx, int *factored);
 int mgx_get_tuning(const char *key, long *value);
 
 /* Per-kernel timing with HIP events on the context stream. */
