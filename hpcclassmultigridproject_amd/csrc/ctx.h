@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -44,8 +45,13 @@ struct Level {
     // factors pitch, zero padded), or null: the passes that take them read
     // the 2-D v1 / v2 from HBM only where no factors exist
     double *sa1 = nullptr, *sb1 = nullptr, *sa2 = nullptr, *sb2 = nullptr;
+    // rows >= vz of v1 and v2 are all zeros (found at upload): the row march
+    // reads them from mgx_ctx::zrow (L2-resident) instead of HBM
+    int vz = 0x7fffffff;
     mgx::Coef coef{};
     double M() const { return double(n + 1) * double(n + 1); }
+    // compulsory bytes of v1 + v2 of this level (the zero rows cost no HBM)
+    double Mv() const { return double(std::min<long>(n + 1, vz)) * double(n + 1); }
     double *U() const { return u[cur]; }
 };
 
@@ -73,6 +79,7 @@ struct mgx_ctx {
     double *dscal = nullptr;      // [0] norm, [2..3] coarse stats (iterations, last norm)
     double *hscal = nullptr;      // pinned host mirror
     double *stage[2] = {nullptr, nullptr};   // reference-layout (N+1)^2 staging
+    double *zrow = nullptr;   // one row of zeros (finest pitch): Level::vz rows read it
     mgxi::Dist *dist = nullptr;   // row-partitioned multi-GPU state (dist.hip)
     // mg_outer's cycle predicted to be the last: its finest level runs the
     // post-smoothing alone, not the cross pass (no next-cycle pre-smoothing)
@@ -133,6 +140,9 @@ int op_vcycle(mgx_ctx *c, int l, double *norm = nullptr, bool store_post = true)
 int op_rhs(mgx_ctx *c);
 int op_residual_norm(mgx_ctx *c, int l, double *norm, double bytes_per_pt = 48.0);
 int build_tower(mgx_ctx *c);
+// Level::vz of levels 1..L-1 from the built tower (the first row from which
+// every row of v1 and v2 is zero)
+int find_zero_rows(mgx_ctx *c);
 // velocity factors of level 0 from host copies of v1 / v2 (rows [r0, r0+rows)
 // of width n+1); false: not separable (or "sep_velocity" off), nothing set
 bool factor_velocity(const double *v1, const double *v2, long n, long r0, long rows, double smin,

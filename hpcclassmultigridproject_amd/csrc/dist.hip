@@ -77,6 +77,7 @@ struct PLevel {
     // level 0: exact velocity factors (sepvel.h) indexed by GLOBAL row / column
     // (full-length arrays, this block's rows filled), or null
     double *sa1 = nullptr, *sb1 = nullptr, *sa2 = nullptr, *sb2 = nullptr;
+    int vz = 0x7fffffff;   // Level::vz (global rows)
     mgx::Coef coef{};
     int nxt() const { return cur == 0 ? 1 : 0; }
     // field pointer offset so that F(a) + r*pitch is global row r
@@ -136,6 +137,11 @@ static int build_dist(mgx_ctx *c, int world, const std::vector<int> &ranks) {
     d->la = plan_la(c->N, c->L, world);
     for (int l = 0; l < d->la; ++l) CHK(plan_check(c->N, l, world));
     HIPCHK(hipHostMalloc(&d->hsum, sizeof(double) * 8));
+    // the zero row the marches read for zero velocity rows: the finest pitch
+    (void)hipFree(c->zrow);
+    c->zrow = nullptr;
+    HIPCHK(hipMalloc(&c->zrow, sizeof(double) * mgx::tower_pitch(c->N)));
+    HIPCHK(hipMemsetAsync(c->zrow, 0, sizeof(double) * mgx::tower_pitch(c->N), c->stream));
     HIPCHK(hipStreamCreateWithFlags(&d->xs, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming));
@@ -366,6 +372,8 @@ static int smooth(mgx_ctx *c, int l, bool prolong, bool restrict_, bool norm) {
             A.partials = c->partials;
             A.norm_out = p.dsum;
             A.norm_sqrt = false;
+            A.zrow = c->zrow;
+            A.vz = L.vz;
             double bytes = 40.0 * k * L.Mown();
             const double Mc = L.Mown() / 4;
             if (pr) bytes += 32.0 * L.Mown() + 8.0 * Mc;
@@ -735,6 +743,7 @@ int dist_upload(mgx_ctx *c, const double *u0, const double *v1, const double *v2
             L.cur = 0;
             L.spec = -1;
             L.zero = false;
+            L.vz = F.vz;
             if (rc == MGX_OK && l == 0) {   // the whole level's velocity factors, if any
                 if (F.sa1)
                     rc = part_factors(L, F.sa1, F.sb1, F.sa2, F.sb2, 0, L.n + 1,
@@ -754,6 +763,7 @@ int dist_upload(mgx_ctx *c, const double *u0, const double *v1, const double *v2
             if (rc) rc = fail(MGX_E_HIP, "dist_upload: copy");
             S.cur = 0;
             S.zero = false;
+            S.vz = F.vz;
         }
     }
     if (rc == MGX_OK && hipStreamSynchronize(c->stream) != hipSuccess)
@@ -882,6 +892,7 @@ static int dist_upload_rows_impl(mgx_ctx *c, const double *const *u0s,
             L.cur = 0;
             L.spec = -1;
             L.zero = false;
+            L.vz = 0x7fffffff;
         }
         PLevel &L = p.lv[0];
         const size_t row = w * sizeof(double), rows = L.hi - L.lo + 1;
@@ -934,6 +945,7 @@ static int dist_upload_rows_impl(mgx_ctx *c, const double *const *u0s,
             L.cur = 0;
             L.spec = -1;
             L.zero = false;
+            L.vz = 0x7fffffff;   // the correct tower has no zero rows to skip
         }
     }
     if (d->world > 1) {

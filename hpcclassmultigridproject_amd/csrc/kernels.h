@@ -37,6 +37,8 @@ void launch_injection(double *dst, long dst_pitch, const double *src, long src_p
 // rows x cols block: dst[I*dst_pitch + J] = src[2I*src_pitch + 2J]
 void launch_injection_rows(double *dst, long dst_pitch, const double *src, long src_pitch,
                            long rows, long cols, hipStream_t s);
+// flags[i] = 1 if row i (columns 0..n) of the pitched field holds a nonzero value
+void launch_row_nonzero(const double *v, long pitch, long n, int *flags, hipStream_t s);
 
 // Sum of squares of the interior of an (n+1)^2 field with row pitch `pitch`,
 // deterministic two-stage reduction; result written to *out (device) as sqrt.
@@ -80,6 +82,11 @@ struct SmoothArgs {
     double *partials;   // NORM
     double *norm_out;   // NORM: sqrt of the sum (norm_sqrt) or the plain sum
     double *rhs_out = nullptr;   // kModeRhsNorm: the computed rhs
+    // rows >= vz of v1 AND v2 are all zeros (the reference tower's coarse
+    // levels, SURVEY K2: 3/4 of every coarse level): the row march reads them
+    // from zrow (one zero row of >= pitch doubles, L2-resident) instead of HBM
+    const double *zrow = nullptr;
+    int vz = 0x7fffffff;
     bool norm_sqrt = true;
     bool norm_accumulate = false;   // NORM: add the plain sum to *norm_out
     // Row-block partitions (multi-GPU): output rows [ra, rb) and rows [lo, hi]

@@ -238,6 +238,19 @@ __global__ __launch_bounds__(256) void k_injection_rows(double *dst, long dpitch
         dst[I * dpitch + J] = src[2 * I * spitch + 2 * J];
 }
 
+__global__ __launch_bounds__(256) void k_row_nonzero(const double *v, long pitch, long n,
+                                                     int *flags) {
+    __shared__ int any;
+    if (threadIdx.x == 0) any = 0;
+    __syncthreads();
+    const double *row = v + (long)blockIdx.x * pitch;
+    int mine = 0;
+    for (long j = threadIdx.x; j <= n; j += 256) mine |= row[j] != 0.0;
+    if (mine) any = 1;   // benign: every writer stores 1
+    __syncthreads();
+    if (threadIdx.x == 0) flags[blockIdx.x] = any;
+}
+
 // Interior sum of squares, rows split over the grid; deterministic per block.
 __global__ __launch_bounds__(256) void k_norm_partial(const double *res, long n, long pitch,
                                                       int rows_per_block, double *partials) {
@@ -696,7 +709,8 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
     const double *__restrict__ uin, double *__restrict__ uout, const double *__restrict__ rhs,
     const double *__restrict__ v1, const double *__restrict__ v2, const double *__restrict__ uc,
     long pitchc, double *__restrict__ rhsc, double *__restrict__ partials, int n, long pitch,
-    MarchRegions reg, long units_per_wg, Coef c, int lo, int hi, double *__restrict__ rhs_out) {
+    MarchRegions reg, long units_per_wg, Coef c, int lo, int hi, double *__restrict__ rhs_out,
+    const double *__restrict__ zrow, int vz) {
     using C = WCfg<K, MODE>;
     constexpr int S = C::S, E = C::E, H = C::H, NR = C::NR, W = C::W;
     // rhs/v prefetch distance in steps (row s+WRV takes the slot of row
@@ -780,11 +794,15 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
         // rhs and v of row R, raw; t = v*h/2 only at the row's first use
         // (scale_rv): scaled here, the multiplies would wait for the loads
         // right after issuing them, and no prefetch distance would help
+        // (rows >= vz: v1 and v2 are zero there, read from the L2-resident
+        // zero row -- a uniform select, the load stays unconditional)
         auto load_rv = [&](int R, RowData &d) {
-            const long o = (long)min(max(R, lo), hi) * pitch;
+            const int Rc = min(max(R, lo), hi);
+            const long o = (long)Rc * pitch;
             if (!C::RHSN) d.r = ld2((rhs + o) + cl);
-            d.x = ld2((v1 + o) + cl);
-            d.y = ld2((v2 + o) + cl);
+            const bool z = Rc >= vz;
+            d.x = ld2((z ? zrow : v1 + o) + cl);
+            d.y = ld2((z ? zrow : v2 + o) + cl);
         };
         auto scale_rv = [&](RowData &d) {
             d.x = make_double2(d.x.x * hh, d.x.y * hh);
@@ -2173,6 +2191,10 @@ void launch_injection_rows(double *dst, long dst_pitch, const double *src, long 
     MGX_LAUNCH(k_injection_rows, g, dim3(256), s, dst, dst_pitch, src, src_pitch, rows, cols);
 }
 
+void launch_row_nonzero(const double *v, long pitch, long n, int *flags, hipStream_t s) {
+    MGX_LAUNCH(k_row_nonzero, dim3((unsigned)(n + 1)), dim3(256), s, v, pitch, n, flags);
+}
+
 int norm_partials_size() { return kNormBlocks; }
 
 void launch_norm(const double *res, long n, long pitch, double *partials, double *out,
@@ -2363,7 +2385,7 @@ static int wsmooth_launch(const SmoothArgs &A, const MarchRegions &reg, double *
                                      WCfg<K, MODE>::E + WCfg<K, MODE>::NR / 2, upw, r);
     MGX_LAUNCH((k_wsmooth<WPB, K, MODE, G>), dim3(grid), dim3(64 * WPB), s, A.uin, A.uout,
                A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch, r, upw,
-               A.c, A.lo, A.hi, A.rhs_out);
+               A.c, A.lo, A.hi, A.rhs_out, A.zrow ? A.zrow : A.v1, A.zrow ? A.vz : 0x7fffffff);
     return (int)grid * WPB;   // NORM partials written
 }
 

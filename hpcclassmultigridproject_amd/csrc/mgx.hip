@@ -166,6 +166,8 @@ int op_smooth(mgx_ctx *c, int l, int sweeps, bool prolong, bool restrict_, bool 
             A.rhs = L.rhs;
             A.v1 = L.v1;
             A.v2 = L.v2;
+            A.zrow = c->zrow;
+            A.vz = L.vz;
             A.n = L.n;
             A.pitch = L.pitch;
             A.c = L.coef;
@@ -187,7 +189,9 @@ int op_smooth(mgx_ctx *c, int l, int sweeps, bool prolong, bool restrict_, bool 
             if (nm) bytes += 48.0 * L.M();
             // compulsory: u (unless zero), rhs, v1, v2 read, u written, the
             // coarse u read (prolong) / coarse rhs written (restrict)
-            const double cbytes = 8.0 * (((mode & mgx::kModeZero) ? 4.0 : 5.0) * L.M() +
+            // (v1 / v2 rows >= vz come from the zero row, not HBM)
+            const double cbytes = 8.0 * (((mode & mgx::kModeZero) ? 2.0 : 3.0) * L.M() +
+                                         2.0 * L.Mv() +
                                          ((pr ? 1 : 0) + (rs ? 1 : 0)) * c->lv[l + 1].M());
             int blocks = 0;
             CHK(launch(c, kind, l, bytes, cbytes,
@@ -657,6 +661,38 @@ int build_tower(mgx_ctx *c) {
     return MGX_OK;
 }
 
+// tuning key "zero_rows": 1 (default) = find_zero_rows at upload; 0 = read
+// every velocity row from HBM
+long g_zero_rows = 1;
+
+int find_zero_rows(mgx_ctx *c) {
+    for (auto &L : c->lv) L.vz = 0x7fffffff;
+    if (c->L < 2 || !g_zero_rows) return MGX_OK;
+    int *dflags = nullptr;
+    const long nmax = c->lv[1].n + 1;
+    HIPCHK(hipMalloc(&dflags, sizeof(int) * 2 * nmax));
+    std::vector<int> h(2 * nmax);
+    int rc = MGX_OK;
+    for (int l = 1; l < c->L && rc == MGX_OK; ++l) {
+        Level &L = c->lv[l];
+        mgx::launch_row_nonzero(L.v1, L.pitch, L.n, dflags, c->stream);
+        mgx::launch_row_nonzero(L.v2, L.pitch, L.n, dflags + nmax, c->stream);
+        if (check_launch("row_nonzero") != MGX_OK ||
+            hipMemcpyAsync(h.data(), dflags, sizeof(int) * 2 * nmax, hipMemcpyDeviceToHost,
+                           c->stream) != hipSuccess ||
+            hipStreamSynchronize(c->stream) != hipSuccess) {
+            rc = fail(MGX_E_HIP, "find_zero_rows");
+            break;
+        }
+        long last = -1;
+        for (long i = 0; i <= L.n; ++i)
+            if (h[i] || h[nmax + i]) last = i;
+        L.vz = (int)(last + 1);
+    }
+    (void)hipFree(dflags);
+    return rc;
+}
+
 void free_ctx(mgx_ctx *c) {
     if (!c) return;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
@@ -675,6 +711,7 @@ void free_ctx(mgx_ctx *c) {
     (void)hipFree(c->dscal);
     (void)hipFree(c->stage[0]);
     (void)hipFree(c->stage[1]);
+    (void)hipFree(c->zrow);
     if (c->hscal) (void)hipHostFree(c->hscal);
     for (auto &r : c->pending) {
         (void)hipEventDestroy(r.e0);
@@ -831,6 +868,9 @@ int mgxi::create_ctx(mgx_ctx **out, long n, int maxlvl, double dt, double nu,
     }
     const size_t flat = sizeof(double) * (n + 1) * (n + 1);
     // (two partial arrays: the cross pass's time-step mode sums two norms)
+    if (hipMalloc(&c->zrow, sizeof(double) * c->lv[0].pitch) != hipSuccess ||
+        hipMemsetAsync(c->zrow, 0, sizeof(double) * c->lv[0].pitch, c->stream) != hipSuccess)
+        return bail(fail(MGX_E_HIP, "hipMalloc (zero row)"));
     if (hipMalloc(&c->partials, 2 * sizeof(double) * mgx::norm_partials_size()) != hipSuccess ||
         hipMalloc(&c->dscal, sizeof(double) * 8) != hipSuccess ||
         hipHostMalloc(&c->hscal, sizeof(double) * 8) != hipSuccess)
@@ -879,6 +919,7 @@ int mgxi::upload_ctx(mgx_ctx *c, const double *u0, const double *v1, const doubl
         c->lv[l].zero = false;
     }
     CHK(build_tower(c));
+    CHK(find_zero_rows(c));
     // exact velocity factors for the finest level's cross pass (host data only;
     // a device upload keeps the 2-D arrays)
     free_level_factors(L);
@@ -1380,6 +1421,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgxi::g_sep_velocity = value;
         return MGX_OK;
     }
+    if (!strcmp(key, "zero_rows")) {
+        if (value != 0 && value != 1) return fail(MGX_E_ARG, "zero_rows must be 0 or 1");
+        mgxi::g_zero_rows = value;
+        return MGX_OK;
+    }
     return fail(MGX_E_ARG, std::string("mgx_set_tuning: unknown key ") + key);
 }
 extern "C" int mgx_get_tuning(const char *key, long *value) {
@@ -1451,6 +1497,10 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "sep_velocity")) {
         *value = mgxi::g_sep_velocity;
+        return MGX_OK;
+    }
+    if (!strcmp(key, "zero_rows")) {
+        *value = mgxi::g_zero_rows;
         return MGX_OK;
     }
     return fail(MGX_E_ARG, std::string("mgx_get_tuning: unknown key ") + key);

@@ -223,7 +223,12 @@ int mgx_set_tuning(const char *key, long value);
  * reference's rotating flow, multigrid.cpp:221-222, is one), is detected at
  * upload and the finest level's cross pass reads its factors instead of the
  * 2-D v1 / v2 (two of its five input streams); 0 = always the 2-D arrays.
- * Bitwise the same results either way. */
+ * Bitwise the same results either way.
+ * "zero_rows": 1 (default) = at upload, the rows from which every row of a
+ * coarse level's v1 and v2 is zero (3/4 of each coarse level of the
+ * reference tower) are found, and the row marches read them from
+ * one L2-resident zero row instead of HBM; 0 = every row from HBM (bitwise
+ * the same results). */
 /* Host only: exact rank-1 factors of v (rows x (n+1), row-major):
  * returns 1 and fills a[rows], b[n+1] with fl(a[i]*b[j]) == v[i][j] (same
  * bits) and every nonzero |v|, |b| still normal after scaling by smin, else 0. */
