@@ -998,6 +998,9 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
 #ifndef MGX_XU
 #define MGX_XU 2
 #endif
+#ifndef MGX_XACOEF
+#define MGX_XACOEF 1
+#endif
 template <int K>
 struct XCfg {
     static constexpr int S = 2 * K;
@@ -1071,6 +1074,8 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     // u 3-4 steps or rhs/v 5 measured no better (N=16384, tools/ab_libs.sh).
     constexpr int XRV = MGX_XRV;
     constexpr int XU = MGX_XU;
+    // A forms each row's coefficients once (MGX_XACOEF; B always does)
+    constexpr bool XACOEF = MGX_XACOEF != 0;
     static_assert(XU >= 1 && XU <= NR - 3, "u prefetch distance");
     // row s+XRV takes the ring slot of row s+XRV-NR, last used by A's norm of
     // row s+1-S
@@ -1283,8 +1288,16 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                     ur[(p + 3) % NR] = make_u(s + 3, up[(p + 3) % NR], (p + 3) & 1);
                     load_u(s + 3 + XU, up[(p + 3 + XU) % NR], (p + 3 + XU) & 1);   // XU ahead
                     make_t((p + 1) % NR);   // row s+1: first used by stage 0 below
+                    if (XACOEF) {
+                        // the row's four coefficients once (as B does), not in
+                        // each of its point's stages
+                        to_coef(rd[(p + 1) % NR], cf[(p + 1) % NR]);
 #pragma unroll
-                    for (int h = 0; h < S; ++h) stage(ur, rd, p, h, s + 1 - h);
+                        for (int h = 0; h < S; ++h) stage_c(p, h, s + 1 - h);
+                    } else {
+#pragma unroll
+                        for (int h = 0; h < S; ++h) stage(ur, rd, p, h, s + 1 - h);
+                    }
                     // hand-off: rhs/v row s+1 (first used above), final u row s+2-S
                     {
                         const RowData &dh = rd[(p + 1) % NR];
@@ -1311,15 +1324,19 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         const RowData &d = rd[iR];
                         const double uW = dpp_shr1(ur[iR].y);
                         const bool rin = r >= a && r < b;
+                        // (with the row's coefficients: the same expressions, bitwise)
+                        auto res0 = [&]() {
+                            if (XACOEF) return res_x(iR, iN, iS, uW);
+                            return res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x, ur[iN].x, uW,
+                                               ur[iS].x, ur[iR].y, c);
+                        };
                         if (GN) {
                             if (rin && keep && r >= 1 && r <= n - 1 && in0) {
-                                const double res = res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x,
-                                                               ur[iN].x, uW, ur[iS].x, ur[iR].y, c);
+                                const double res = res0();
                                 acc += res * res;
                             }
                         } else {   // acc + 0.0 == acc (acc >= +0): a select, no branch
-                            const double r0 = res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x, ur[iN].x,
-                                                          uW, ur[iS].x, ur[iR].y, c);
+                            const double r0 = res0();
                             acc += (keep && rin) ? r0 * r0 : 0.0;
                         }
                     }
