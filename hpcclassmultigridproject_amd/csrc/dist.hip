@@ -92,6 +92,9 @@ struct Part {
     std::vector<PLevel> lv;   // levels 0..la-1
     mgx_ctx *sub = nullptr;   // levels la..L-1, full, replicated
     double *dsum = nullptr;   // device scalar: this rank's partial sum of squares
+    double *partials = nullptr;   // this part's norm partials (a split pass keeps them
+                                  // between its two launches while other parts run)
+    hipEvent_t xe0 = nullptr;     // profiling: the start of a split pass
 };
 
 struct Dist {
@@ -121,6 +124,7 @@ void dist_free(mgx_ctx *c) {
         }
         if (p.sub) free_ctx(p.sub);
         (void)hipFree(p.dsum);
+        (void)hipFree(p.partials);
     }
     if (d->comm) (void)ncclCommDestroy(d->comm);
     if (d->xs) (void)hipStreamDestroy(d->xs);
@@ -169,6 +173,7 @@ static int build_dist(mgx_ctx *c, int world, const std::vector<int> &ranks) {
         so.device = -1;
         CHK(create_ctx(&p.sub, c->N >> d->la, c->L - d->la, c->dt, c->nu, &so, c->stream));
         HIPCHK(hipMalloc(&p.dsum, sizeof(double) * 8));
+        HIPCHK(hipMalloc(&p.partials, sizeof(double) * 2 * mgx::norm_partials_size()));
         d->parts.push_back(p);
     }
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -369,7 +374,7 @@ static int smooth(mgx_ctx *c, int l, bool prolong, bool restrict_, bool norm) {
                     A.pitchc = Cl.pitch;
                 }
             }
-            A.partials = c->partials;
+            A.partials = p.partials;
             A.norm_out = p.dsum;
             A.norm_sqrt = false;
             A.zrow = c->zrow;
@@ -444,17 +449,19 @@ static void dist_drop_spec(mgx_ctx *c) {
 // is made ready on level 1 and the per-rank norm sums are reduced by the caller.
 //
 // dist_overlap = 1: the exchange goes on the second stream (forked after the
-// work that produced the sent rows) while the compute stream runs the pass
-// over rows [ra+16, rb-16) -- whose cone [ra+2, rb-2) and coarse parents are
-// all owned, so it needs no ghost row -- then, after the exchange, the two
-// 16-row bands next to the ghosts (norm partial sums accumulated).  Outputs,
-// u_pre / u_post / coarse rhs, are the same rows either way: bitwise.
+// work that produced the sent rows) while the compute stream runs the pass's
+// unguarded interior march over rows [ra+16, rb-16) -- whose cone [ra+2, rb-2)
+// and coarse parents are all owned, so it needs no ghost row -- and the pass's
+// edge launch, which the split pass always has (boundary strips, global
+// bands), takes the two 16-row bands next to the ghosts too, after the join
+// (launch_xsmooth phases 1 and 2: no launch more than the plain pass).
+// Outputs, u_pre / u_post / coarse rhs, are the same rows either way: bitwise.
 static int dist_cross(mgx_ctx *c, bool store_post) {
     Dist *d = c->dist;
     const int G = kGhostFine;
     const int k = c->opt.nsmooth;
     bool ov = g_dist_overlap != 0 && d->world > 1;
-    for (auto &p : d->parts) ov = ov && p.lv[0].rb - p.lv[0].ra >= 4 * G;
+    for (auto &p : d->parts) ov = ov && p.lv[0].rb - p.lv[0].ra >= 4 * G && p.lv[0].coef.dgs > 0;
     auto xs = {XF{0, kU}, XF{1, kU}};
     auto x0 = {XF{0, kU}};
     if (ov) {
@@ -474,8 +481,8 @@ static int dist_cross(mgx_ctx *c, bool store_post) {
     } else {
         CHK(exchange(c, 1 < d->la ? xs : x0));
     }
-    // one launch of the pass over owned rows [ra, rb) of part p
-    auto pass = [&](Part &p, int P, int Q, int ra, int rb, bool accumulate) -> int {
+    // one launch (phase 1 / 2) or both of the pass over owned rows [ra, rb) of part p
+    auto pass = [&](Part &p, int P, int Q, int phase, int done) -> int {
         PLevel &L = p.lv[0];
         mgx::XArgs A;
         A.uin = L.U();
@@ -484,7 +491,6 @@ static int dist_cross(mgx_ctx *c, bool store_post) {
         A.rhs = L.F(L.rhs);
         A.v1 = L.F(L.v1);
         A.v2 = L.F(L.v2);
-        double Mc;
         if (1 < d->la) {
             PLevel &Cl = p.lv[1];
             A.uc = Cl.U();
@@ -496,12 +502,10 @@ static int dist_cross(mgx_ctx *c, bool store_post) {
             A.rhsc = Cl.rhs;
             A.pitchc = Cl.pitch;
         }
-        const double Mown = double(rb - ra) * double(L.n + 1);
-        Mc = Mown / 4;
-        A.partials = c->partials;
+        const double Mown = L.Mown(), Mc = Mown / 4;
+        A.partials = p.partials;
         A.norm_out = p.dsum;
         A.norm_sqrt = false;
-        A.norm_accumulate = accumulate;
         A.n = L.n;
         A.pitch = L.pitch;
         A.c = L.coef;
@@ -510,19 +514,40 @@ static int dist_cross(mgx_ctx *c, bool store_post) {
         A.sb1 = L.sb1;
         A.sa2 = L.sa2;
         A.sb2 = L.sb2;
-        A.ra = ra;
-        A.rb = rb;
+        A.ra = L.ra;
+        A.rb = L.rb;
         A.lo = L.lo;
         A.hi = L.hi;
-        if (rb - ra < 4 * G) A.min_rows = 8;   // a band: many short segments
-        const double bytes = (32.0 + 40.0 * k + 48.0 + 40.0 * k + 40.0) * Mown + 32.0 * Mc;
+        A.band = phase ? G : 0;
+        A.phase = phase;
+        A.partials_done = done;
+        // (a split pass's bytes and time are counted on its second launch)
+        const double bytes =
+            phase == 1 ? 0.0 : (32.0 + 40.0 * k + 48.0 + 40.0 * k + 40.0) * Mown + 32.0 * Mc;
         const double cbytes =
-            8.0 * ((store_post ? 6.0 : 5.0) * Mown - (L.sa1 ? 2.0 * Mown : 0.0) + 2.0 * Mc);
+            phase == 1 ? 0.0
+                       : 8.0 * ((store_post ? 6.0 : 5.0) * Mown - (L.sa1 ? 2.0 * Mown : 0.0) +
+                                2.0 * Mc);
         int blocks = 0;
-        CHK(launch(c, MGX_K_XSMOOTH, 0, bytes, cbytes,
-                   [&] { blocks = mgx::launch_xsmooth(A, k, c->stream); }));
+        if (phase == 0) {
+            CHK(launch(c, MGX_K_XSMOOTH, 0, bytes, cbytes,
+                       [&] { blocks = mgx::launch_xsmooth(A, k, c->stream); }));
+        } else {   // a split pass is timed from its first launch to its second
+            const bool rec = c->prof == 1 || c->prof == 2;
+            hipEvent_t &e0 = p.xe0;
+            if (phase == 1) e0 = rec ? take_event(c) : nullptr;
+            if (phase == 1 && e0) HIPCHK(hipEventRecord(e0, c->stream));
+            blocks = mgx::launch_xsmooth(A, k, c->stream);
+            CHK(check_launch("launch_xsmooth"));
+            hipEvent_t e1 = (phase == 2 && e0) ? take_event(c) : nullptr;
+            if (e1) {
+                HIPCHK(hipEventRecord(e1, c->stream));
+                c->pending.push_back({MGX_K_XSMOOTH, 0, bytes, cbytes, e0, e1});
+                e0 = nullptr;
+            }
+        }
         if (blocks < 0) return fail(MGX_E_ARG, "launch_xsmooth: unsupported sweeps / block");
-        return MGX_OK;
+        return blocks;
     };
     std::vector<std::pair<int, int>> bufs;
     for (auto &p : d->parts) {
@@ -534,22 +559,19 @@ static int dist_cross(mgx_ctx *c, bool store_post) {
     }
     if (!ov) {
         for (size_t i = 0; i < d->parts.size(); ++i) {
-            PLevel &L = d->parts[i].lv[0];
-            CHK(pass(d->parts[i], bufs[i].first, bufs[i].second, L.ra, L.rb, false));
+            const int r = pass(d->parts[i], bufs[i].first, bufs[i].second, 0, 0);
+            if (r < 0) return r;
         }
     } else {
-        // bands start at even rows (the pass's row parity / restriction)
+        std::vector<int> done(d->parts.size());
         for (size_t i = 0; i < d->parts.size(); ++i) {
-            PLevel &L = d->parts[i].lv[0];
-            const int top = (L.rb - G) & ~1;
-            CHK(pass(d->parts[i], bufs[i].first, bufs[i].second, L.ra + G, top, false));
+            done[i] = pass(d->parts[i], bufs[i].first, bufs[i].second, 1, 0);
+            if (done[i] < 0) return done[i];
         }
         HIPCHK(hipStreamWaitEvent(c->stream, d->ev_join, 0));
         for (size_t i = 0; i < d->parts.size(); ++i) {
-            PLevel &L = d->parts[i].lv[0];
-            const int top = (L.rb - G) & ~1;
-            CHK(pass(d->parts[i], bufs[i].first, bufs[i].second, L.ra, L.ra + G, true));
-            CHK(pass(d->parts[i], bufs[i].first, bufs[i].second, top, L.rb, true));
+            const int r = pass(d->parts[i], bufs[i].first, bufs[i].second, 2, done[i]);
+            if (r < 0) return r;
         }
     }
     for (size_t i = 0; i < d->parts.size(); ++i) {
@@ -631,7 +653,7 @@ int dist_residual_norm(mgx_ctx *c, double *norm) {
         PLevel &L = p.lv[0];
         CHK(launch(c, MGX_K_RESNORM, 0, 48.0 * L.Mown(), 32.0 * L.Mown(), [&] {
             mgx::launch_residual_norm(L.U(), L.F(L.rhs), L.F(L.v1), L.F(L.v2), L.n, L.pitch,
-                                      L.coef, c->partials, p.dsum, c->stream, L.ra, L.rb,
+                                      L.coef, p.partials, p.dsum, c->stream, L.ra, L.rb,
                                       /*take_sqrt=*/false);
         }));
     }
@@ -672,7 +694,7 @@ int dist_rhs_norm(mgx_ctx *c, double *res0) {
         PLevel &L = p.lv[0];
         CHK(launch(c, MGX_K_RHS, 0, 80.0 * L.Mown(), 32.0 * L.Mown(), [&] {
             mgx::launch_rhs_norm(L.F(L.rhs), L.U(), L.F(L.v1), L.F(L.v2), L.n, L.pitch, L.coef,
-                                 c->partials, p.dsum, c->stream, L.ra, L.rb,
+                                 p.partials, p.dsum, c->stream, L.ra, L.rb,
                                  /*take_sqrt=*/false);
         }));
     }

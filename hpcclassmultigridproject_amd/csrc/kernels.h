@@ -126,6 +126,12 @@ struct XArgs {
     // row R, column c; sb zero-padded to the pitch), v2 likewise; all four set
     // = the pass reads rhs and u only (the 2-D v1 / v2 are not touched)
     const double *sa1 = nullptr, *sb1 = nullptr, *sa2 = nullptr, *sb2 = nullptr;
+    // Split pass (the overlapped ghost exchange of a row block): band > 0 moves
+    // rows [ra, ra+band) and [rb-band, rb) from the unguarded interior march to
+    // the edge launch; phase 1 = the interior march only (returns its partials
+    // count, no norm), phase 2 = the edge launch only, its partials written
+    // after the first `partials_done` and the norm taken over both; 0 = both.
+    int band = 0, phase = 0, partials_done = 0;
 };
 int launch_xsmooth(const XArgs &a, int sweeps, hipStream_t s);
 // whether launch_xsmooth supports rhs_next on a whole level of size n

@@ -704,7 +704,15 @@ __device__ __forceinline__ double rhs_point_t(double t1, double t2, double u, do
 
 // G = false: the unguarded march (interior strips, rows [TOP, n+1-BOT) of
 // WCfg: no per-stage predicates), G = true: guarded (see k_xsmooth).
-template <int WPB, int K, int MODE, bool G>
+// PD: the diagonal is positive (every nu <= 0): the shorter division (div_diag).
+// MGX_WCOEF: each row's four coefficients are formed once, at its first stage
+// (as in k_xsmooth), instead of in every stage of its points.
+// (2: only the x-neighbour pair cn, cs, from t1 -- half the registers of all
+// four -- the y pair from t2 in every stage)
+#ifndef MGX_WCOEF
+#define MGX_WCOEF 2
+#endif
+template <int WPB, int K, int MODE, bool G, bool PD = false>
 __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
     const double *__restrict__ uin, double *__restrict__ uout, const double *__restrict__ rhs,
     const double *__restrict__ v1, const double *__restrict__ v2, const double *__restrict__ uc,
@@ -816,11 +824,38 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
 
         double2 ur[NR];
         RowData rd[NR];
+        constexpr bool WC = MGX_WCOEF == 1 && !C::RHSN;
+        constexpr bool WH = MGX_WCOEF == 2 && !C::RHSN;   // half: cn, cs stored
+        CoefRow cf[NR];
 #pragma unroll
         for (int q = 0; q < NR; ++q) {
             ur[q] = make_double2(0.0, 0.0);
             rd[q].r = rd[q].x = rd[q].y = make_double2(0.0, 0.0);
+            const double2 z = make_double2(0.0, 0.0);
+            cf[q] = CoefRow{z, z, z, z};
         }
+        // gs.cpp:126-129 coefficients of a row's two points from t1, t2
+        auto to_coef = [&](const RowData &d, CoefRow &k) {
+            k.cn = make_double2(c.rr * (c.nu - d.x.x), c.rr * (c.nu - d.x.y));
+            k.cw = make_double2(c.rr * (c.nu - d.y.x), c.rr * (c.nu - d.y.y));
+            k.cs = make_double2(c.rr * (d.x.x + c.nu), c.rr * (d.x.y + c.nu));
+            k.ce = make_double2(c.rr * (d.y.x + c.nu), c.rr * (d.y.y + c.nu));
+        };
+        // residual (gs.cpp:75 term order) of the row in slot iR, column c0 / c0+1
+        auto res_cx = [&](const int iR, const int iN, const int iS, const double uW) {
+            const CoefRow &k = cf[iR];
+            const double cw = MGX_WCOEF == 2 ? c.rr * (c.nu - rd[iR].y.x) : k.cw.x;
+            const double ce = MGX_WCOEF == 2 ? c.rr * (rd[iR].y.x + c.nu) : k.ce.x;
+            return rd[iR].r.x - (c.dgs * ur[iR].x + k.cn.x * ur[iN].x + cw * uW +
+                                 k.cs.x * ur[iS].x + ce * ur[iR].y);
+        };
+        auto res_cy = [&](const int iR, const int iN, const int iS, const double uE) {
+            const CoefRow &k = cf[iR];
+            const double cw = MGX_WCOEF == 2 ? c.rr * (c.nu - rd[iR].y.y) : k.cw.y;
+            const double ce = MGX_WCOEF == 2 ? c.rr * (rd[iR].y.y + c.nu) : k.ce.y;
+            return rd[iR].r.y - (c.dgs * ur[iR].y + k.cn.y * ur[iN].y + cw * ur[iR].x +
+                                 k.cs.y * ur[iS].y + ce * uE);
+        };
         // prologue (s == 0 mod NR): u rows s..s+2 in the ring, s+3 / s+4 in
         // flight (sets 1 / 0), rhs/v rows s+1, s+2 loaded
 #pragma unroll
@@ -882,6 +917,13 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                 load_u(s + 5, up[(p + 1) & 1], (p + 1) & 1);
                 // t of the row first used in this step: s+2 (RHSN), else s+1
                 scale_rv(rd[(p + (C::RHSN ? 2 : 1)) % NR]);
+                if (WC) to_coef(rd[(p + 1) % NR], cf[(p + 1) % NR]);
+                if (WH) {   // cn, cs of row s+1 from t1 (gs.cpp:128-129's cc, dd)
+                    const RowData &d1 = rd[(p + 1) % NR];
+                    CoefRow &k1 = cf[(p + 1) % NR];
+                    k1.cn = make_double2(c.rr * (c.nu - d1.x.x), c.rr * (c.nu - d1.x.y));
+                    k1.cs = make_double2(c.rr * (d1.x.x + c.nu), c.rr * (d1.x.y + c.nu));
+                }
                 // rows s+1..s+3 are still original u: rhs of row s+2
                 if (C::RHSN) rhs_norm(s + 2, (p + 2) % NR, (p + 1) % NR, (p + 3) % NR);
                 // (2) the S smoothing stages
@@ -898,16 +940,42 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                     // coefficient CSE: it would need more VGPRs, see k_xsmooth)
                     Coef cg = c;
                     if (!G) asm volatile("" : "+s"(cg.nu));
+                    const CoefRow &k = cf[iR];
                     if (cs == 0) {
                         const double uW = dpp_shr1(ur[iR].y);   // column c0-1
-                        if (!G || (inr && in0))
-                            ur[iR].x = gs_point_t(d.r.x, d.x.x, d.y.x, ur[iN].x, uW, ur[iS].x,
-                                                  ur[iR].y, cg);
+                        if (!G || (inr && in0)) {
+                            if (WH)
+                                ur[iR].x = div_diag<PD>(d.r.x - k.cn.x * ur[iN].x -
+                                                            cg.rr * (cg.nu - d.y.x) * uW -
+                                                            k.cs.x * ur[iS].x -
+                                                            cg.rr * (d.y.x + cg.nu) * ur[iR].y,
+                                                        c);
+                            else if (WC)
+                                ur[iR].x = div_diag<PD>(d.r.x - k.cn.x * ur[iN].x - k.cw.x * uW -
+                                                            k.cs.x * ur[iS].x - k.ce.x * ur[iR].y,
+                                                        c);
+                            else
+                                ur[iR].x = gs_point_t<PD>(d.r.x, d.x.x, d.y.x, ur[iN].x, uW,
+                                                          ur[iS].x, ur[iR].y, cg);
+                        }
                     } else {
                         const double uE = dpp_shl1(ur[iR].x);   // column c0+2
-                        if (!G || (inr && in1))
-                            ur[iR].y = gs_point_t(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x,
-                                                  ur[iS].y, uE, cg);
+                        if (!G || (inr && in1)) {
+                            if (WH)
+                                ur[iR].y = div_diag<PD>(d.r.y - k.cn.y * ur[iN].y -
+                                                            cg.rr * (cg.nu - d.y.y) * ur[iR].x -
+                                                            k.cs.y * ur[iS].y -
+                                                            cg.rr * (d.y.y + cg.nu) * uE,
+                                                        c);
+                            else if (WC)
+                                ur[iR].y = div_diag<PD>(d.r.y - k.cn.y * ur[iN].y -
+                                                            k.cw.y * ur[iR].x - k.cs.y * ur[iS].y -
+                                                            k.ce.y * uE,
+                                                        c);
+                            else
+                                ur[iR].y = gs_point_t<PD>(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x,
+                                                          ur[iS].y, uE, cg);
+                        }
                     }
                 }
                 // (3) row s+2-S is final
@@ -924,37 +992,39 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                     const int iS = (p + 2 - S + 2 * NR) % NR;
                     const RowData &d = rd[iR];
                     const double uW = dpp_shr1(ur[iR].y);
+                    // (the same expressions from the row's coefficients, bitwise)
+                    auto rx = [&]() {
+                        if (WC || WH) return res_cx(iR, iN, iS, uW);
+                        return res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x, ur[iN].x, uW, ur[iS].x,
+                                           ur[iR].y, c);
+                    };
                     if (C::REST) {
                         if (((p + 1 - S) & 1) == 0 && r >= a && r < b && keep &&
                             (!G || (r >= 1 && r <= n - 2 && in0 && c0 <= n - 2))) {
-                            const double res = res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x,
-                                                           ur[iN].x, uW, ur[iS].x, ur[iR].y, c);
+                            const double res = rx();
                             (rhsc + (long)(r >> 1) * pitchc)[c0 >> 1] = res;
                         }
                     } else {
                         const double uE = dpp_shl1(ur[iR].x);
+                        auto ry = [&]() {
+                            if (WC || WH) return res_cy(iR, iN, iS, uE);
+                            return res_point_t(d.r.y, d.x.y, d.y.y, ur[iR].y, ur[iN].y, ur[iR].x,
+                                               ur[iS].y, uE, c);
+                        };
                         if (!G) {   // acc + 0.0 == acc (acc >= +0): selects, no branch
                             if (r >= a && r < b) {
-                                const double r0 = res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x,
-                                                              ur[iN].x, uW, ur[iS].x, ur[iR].y,
-                                                              c);
-                                const double r1 = res_point_t(d.r.y, d.x.y, d.y.y, ur[iR].y,
-                                                              ur[iN].y, ur[iR].x, ur[iS].y, uE,
-                                                              c);
+                                const double r0 = rx();
+                                const double r1 = ry();
                                 acc += keep ? r0 * r0 : 0.0;
                                 acc += keep ? r1 * r1 : 0.0;
                             }
                         } else if (keep && r >= a && r < b && r >= 1 && r <= n - 1) {
                             if (in0) {
-                                const double res = res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x,
-                                                               ur[iN].x, uW, ur[iS].x,
-                                                               ur[iR].y, c);
+                                const double res = rx();
                                 acc += res * res;
                             }
                             if (in1) {
-                                const double res = res_point_t(d.r.y, d.x.y, d.y.y, ur[iR].y,
-                                                               ur[iN].y, ur[iR].x, ur[iS].y,
-                                                               uE, c);
+                                const double res = ry();
                                 acc += res * res;
                             }
                         }
@@ -2378,9 +2448,9 @@ static unsigned plan_march(const MarchRegions &reg, int wpb, long slots, long mi
     return (unsigned)(ng * ((rows + B - 1) / B));
 }
 
-template <int WPB, int K, int MODE, bool G>
-static int wsmooth_launch(const SmoothArgs &A, const MarchRegions &reg, double *partials,
-                          long max_wgs, hipStream_t s) {
+template <int WPB, int K, int MODE, bool G, bool PD>
+static int wsmooth_launch_pd(const SmoothArgs &A, const MarchRegions &reg, double *partials,
+                             long max_wgs, hipStream_t s) {
     const long total = reg.pre[reg.count];
     if (total <= 0) return 0;
     static int slots = 0;   // resident workgroups of this instantiation
@@ -2388,7 +2458,7 @@ static int wsmooth_launch(const SmoothArgs &A, const MarchRegions &reg, double *
         int dev = 0, cus = 0, per = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_wsmooth<WPB, K, MODE, G>,
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_wsmooth<WPB, K, MODE, G, PD>,
                                                            64 * WPB, 0);
         slots = std::max(1, cus) * std::max(1, per);
     }
@@ -2400,10 +2470,17 @@ static int wsmooth_launch(const SmoothArgs &A, const MarchRegions &reg, double *
     // strips); the same per rank on 8 row blocks
     const unsigned grid = plan_march(reg, WPB, slots, march_min_rows(), max_wgs,
                                      WCfg<K, MODE>::E + WCfg<K, MODE>::NR / 2, upw, r);
-    MGX_LAUNCH((k_wsmooth<WPB, K, MODE, G>), dim3(grid), dim3(64 * WPB), s, A.uin, A.uout,
+    MGX_LAUNCH((k_wsmooth<WPB, K, MODE, G, PD>), dim3(grid), dim3(64 * WPB), s, A.uin, A.uout,
                A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch, r, upw,
                A.c, A.lo, A.hi, A.rhs_out, A.zrow ? A.zrow : A.v1, A.zrow ? A.vz : 0x7fffffff);
     return (int)grid * WPB;   // NORM partials written
+}
+// the short division when the diagonal is positive (every nu <= 0)
+template <int WPB, int K, int MODE, bool G>
+static int wsmooth_launch(const SmoothArgs &A, const MarchRegions &reg, double *partials,
+                          long max_wgs, hipStream_t s) {
+    if (A.c.dgs > 0) return wsmooth_launch_pd<WPB, K, MODE, G, true>(A, reg, partials, max_wgs, s);
+    return wsmooth_launch_pd<WPB, K, MODE, G, false>(A, reg, partials, max_wgs, s);
 }
 
 // One guarded launch over the whole level.  (The interior / edge split that
@@ -2489,12 +2566,21 @@ constexpr int kXTileRows = 16;
 // The cross pass of a short row block: the unguarded march over the interior
 // strips x rows [ma, mb), k_xtile over the boundary strips and the top /
 // bottom bands (or over everything, when [ma, mb) is short).
+// the unguarded march's row margins, widened by the split pass's bands
+template <int K>
+static void xmargins(const XArgs &A, int ra, int rb, int &top, int &bot) {
+    using X = XCfg<K>;
+    top = std::max(X::TOP, ra + A.band);
+    bot = std::max(X::BOT, (int)A.n + 1 - rb + A.band);
+}
+
 template <int WPB, int K>
 static int xsmooth_tiled(const XArgs &A, int ra, int rb, int lo, int hi, hipStream_t s) {
     using X = XCfg<K>;
     const long n = A.n;
-    int si0, si1, ma, mb;
-    march_split(n, X::W, X::H, ra, rb, X::TOP, X::BOT, si0, si1, ma, mb);
+    int si0, si1, ma, mb, top, bot;
+    xmargins<K>(A, ra, rb, top, bot);
+    march_split(n, X::W, X::H, ra, rb, top, bot, si0, si1, ma, mb);
     TileRegions t{};
     const bool inner_march = si1 > si0 && mb - ma >= kXTileAllRows;
     if (inner_march) {
@@ -2509,13 +2595,14 @@ static int xsmooth_tiled(const XArgs &A, int ra, int rb, int lo, int hi, hipStre
     const int tiles = t.pre[t.count];
     // one norm partial per tile; the inner march writes at most kNormBlocks / 2
     if (tiles > kNormBlocks / 2) return -2;   // too many: the caller marches the edges
-    int pm = 0;
-    if (inner_march) {
+    int pm = A.phase == 2 ? A.partials_done : 0;
+    if (inner_march && A.phase != 2) {
         MarchRegions inner{};
         add_region<WPB>(inner, si0, si1, ma, mb);
         pm = xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, A.min_rows,
                                            kNormBlocks / (2 * WPB) / 2, s);
     }
+    if (A.phase == 1) return pm;
     if (tiles > 0)
         MGX_LAUNCH((k_xtile<K, kXTileRows>), dim3((unsigned)tiles), dim3(256), s, A.uin, A.upre,
                    A.upost, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, A.partials + pm, (int)n,
@@ -2560,14 +2647,20 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
     MarchRegions inner, edge, unused;
     // the unguarded kernel's division assumes d > 0 (div_diag<true>)
     const bool split = g_xfast != 0 && A.c.dgs > 0;
+    if (A.phase != 0 && !split) return -1;   // a split pass needs the split kernels
     if (split && rb - ra <= g_xtile_max_rows) {
         const int r = xsmooth_tiled<WPB, K>(A, ra, rb, lo, hi, s);
         if (r != -2) return r;
     }
-    march_regions<WPB>(n, X::W, X::H, ra, rb, X::TOP, X::BOT, split, inner, unused);
-    march_regions<1>(n, X::W, X::H, ra, rb, X::TOP, X::BOT, split, unused, edge);
-    const int pm = xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, A.min_rows,
-                                                 kNormBlocks / (2 * WPB) / 2, s);
+    int top, bot;
+    xmargins<K>(A, ra, rb, top, bot);
+    march_regions<WPB>(n, X::W, X::H, ra, rb, top, bot, split, inner, unused);
+    march_regions<1>(n, X::W, X::H, ra, rb, top, bot, split, unused, edge);
+    const int pm = A.phase == 2 ? A.partials_done
+                                : xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi,
+                                                                A.min_rows,
+                                                                kNormBlocks / (2 * WPB) / 2, s);
+    if (A.phase == 1) return pm;
     const int pe = xsmooth_launch<1, K, true>(A, edge, A.partials + pm, lo, hi,
                                               std::min(32, A.min_rows), kNormBlocks / 2 / 2, s);
     return pm + pe;
@@ -2584,6 +2677,7 @@ int launch_xsmooth(const XArgs &A, int sweeps, hipStream_t s) {
         case 3: blocks = xsmooth_inst<4, 3>(A, s); break;
         default: return -1;
     }
+    if (A.phase == 1) return blocks;   // the norm comes with phase 2
     if (blocks > 0)
         MGX_LAUNCH(k_norm_final, dim3(1), dim3(kFinalThreads), s, (const double *)A.partials,
                    blocks, A.norm_out, A.norm_accumulate ? 2 : A.norm_sqrt ? 1 : 0);
