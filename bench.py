@@ -121,8 +121,13 @@ def parse():
                          "partitioning the same grid")
     ap.add_argument("--row-upload", choices=["auto", "on", "off"], default="auto",
                     help="multi-GPU: each rank builds only its rows (auto: N > 16384)")
+    ap.add_argument("--overlap", choices=["auto", "0", "1", "2"], default="auto",
+                    help="N > 1: dist_overlap for the timed region; auto = price 0 / 1 / 2 "
+                         "in the warm-up (3 cycles each, max over ranks) and keep the fastest")
     ap.add_argument("--rccl-check", type=int, default=1,
                     help="N > 1: first check libmgx's RCCL path bitwise vs one GPU (N=4096)")
+    ap.add_argument("--no-generic", action="store_true",
+                    help="skip the comparison run with the generic (2-D) velocity path")
     ap.add_argument("--no-profile", action="store_true",
                     help="do not record per-kernel HIP events in the timed region")
     ap.add_argument("--sweep", nargs=2, type=int, metavar=("NMIN", "NMAX"),
@@ -317,6 +322,36 @@ def main():
     for _ in range(args.warmup):
         mg.run_cycles(1)
     mg.synchronize()
+
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    overlap_ab = None
+    if world > 1:
+        # price the exchange schedules on this machine (untimed warm-up): the
+        # early level-0 exchange behind the coarse levels pays over xGMI but not
+        # on one GPU's virtual ranks
+        if args.overlap == "auto":
+            overlap_ab = {}
+            for ov in (0, 1, 2):
+                _lib.set_tuning("dist_overlap", ov)
+                mg.run_cycles(1)
+                mg.synchronize()
+                barrier()
+                t0 = time.perf_counter()
+                mg.run_cycles(3)
+                mg.synchronize()
+                overlap_ab[ov] = round(max_over_ranks(time.perf_counter() - t0) / 3 * 1e3, 4)
+            best_ov = min(overlap_ab, key=overlap_ab.get)
+        else:
+            best_ov = int(args.overlap)
+        _lib.set_tuning("dist_overlap", best_ov)
+        mg.run_cycles(1)
+        mg.synchronize()
     mg.profile_reset()
     if not args.no_profile:
         # HIP events around the finest-level launches only (the dominant
@@ -332,11 +367,7 @@ def main():
     mg.synchronize()
     barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(time.perf_counter() - t0)
 
     # dominant kernel = the finest-level (kind) with the largest device time
     # in the timed region
@@ -369,7 +400,41 @@ def main():
                     if nl:
                         kernels[name][f"L{lvl}_ms_per_step"] = round(msl / prof_steps, 4)
         mg.profile(False)
+    import ctypes
+    fac = ctypes.c_int(0)
+    if world == 1:
+        _lib.check(_lib.lib().mgx_velocity_factored(mg.handle, ctypes.byref(fac)))
     mg.close()
+
+    # the same V-cycle with the generic velocity path (2-D v1 / v2 on every
+    # row of every level: sep_velocity = zero_rows = 0), for comparison: the
+    # headline reads the reference flow's exact rank-1 factors on level 0 and
+    # skips the coarse levels' all-zero velocity rows
+    generic = None
+    if world == 1 and not args.no_generic:
+        keys = {k: _lib.get_tuning(k) for k in ("sep_velocity", "zero_rows")}
+        try:
+            for k in keys:
+                _lib.set_tuning(k, 0)
+            g = pkg.Multigrid(N, L, dt, nu, nsmooth=args.nsmooth, device=local,
+                              smoother=args.smoother, fuse=args.fuse, tower_mode=tower)
+            u0, v1, v2 = pkg.init_problem(N, nthreads=16)
+            g.upload(u0, v1, v2)
+            del u0, v1, v2
+            g.rhs()
+            g.run_cycles(2)
+            g.synchronize()
+            t0 = time.perf_counter()
+            g.run_cycles(args.steps)
+            g.synchronize()
+            gms = (time.perf_counter() - t0) / args.steps * 1e3
+            g.close()
+            generic = {"ms_per_step": round(gms, 4),
+                       "value": (N - 1) ** 2 / (gms * 1e-3),
+                       "note": "sep_velocity=0, zero_rows=0: every velocity row read from HBM"}
+        finally:
+            for k, v in keys.items():
+                _lib.set_tuning(k, v)
 
     roof = None
     if best:
@@ -434,9 +499,15 @@ def main():
                    "parallelism": (f"row-partition x{world} on levels 0..{la - 1}, "
                                    f"levels {la}..{L - 1} replicated" if world > 1
                                    else "single"),
+                   "dist_overlap": _lib.get_tuning("dist_overlap") if world > 1 else None,
+                   "overlap_ms_per_cycle": overlap_ab,
                    "last_residual": res},
         "roofline": roof,
         "kernels": kernels,
+        "velocity": ("level 0: exact rank-1 factors (sep_velocity); coarse levels: all-zero "
+                     "rows from one L2-resident row (zero_rows)" if fac.value else
+                     "2-D arrays"),
+        "generic_velocity_path": generic,
     }
     if rccl_check is not None:
         out["rccl_parity"] = rccl_check

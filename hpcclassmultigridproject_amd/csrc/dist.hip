@@ -36,9 +36,17 @@
 namespace mgxi {
 
 long g_dist_min_rows = 256;
-// tuning key "dist_overlap": 1 = the finest level's ghost exchange runs on a
-// second stream while the cross-cycle pass updates the rows whose cone stays
-// inside the block; the two ghost-dependent bands follow the exchange
+// tuning key "dist_overlap": 1 = the finest level's u ghost rows are exchanged
+// on a second stream as soon as the pass that wrote them ends, hidden behind
+// the coarse levels of the V-cycle (the level-0 pass that reads them waits
+// for it); 2 = that, and the cross pass's remaining exchange (level-1 u) on
+// the second stream too, beside the pass's interior march (the bands next to
+// the ghosts go to its edge launch); 0 (default) = every exchange on the
+// compute stream.  On virtual ranks (one GPU) the early exchange's copies
+// compete with the level passes for the same chip and cost 2-3 %; over xGMI
+// it takes the level-0 exchange (2 x 16 rows, ~4 MB per rank) off the critical
+// path -- bench.py prices 0 / 1 / 2 on the N-GPU run itself and keeps the
+// fastest for its timed region
 long g_dist_overlap = 0;
 
 // the partition / exchange plan (plan.h, host-only)
@@ -107,11 +115,16 @@ struct Dist {
     // dist_overlap: ghost exchanges on a second stream beside the interior pass
     hipStream_t xs = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // dist_overlap: level-0 u buffer whose ghost rows the side stream has
+    // exchanged (or is exchanging: early_pending) since it was last written, or -1
+    int early_buf = -1;
+    bool early_pending = false;
 };
 
 void dist_free(mgx_ctx *c) {
     Dist *d = c->dist;
     if (!d) return;
+    if (d->xs) (void)hipStreamSynchronize(d->xs);   // an early exchange may still run
     for (auto &p : d->parts) {
         for (auto &L : p.lv) {
             (void)hipFree(L.u[0]);
@@ -183,9 +196,9 @@ static int build_dist(mgx_ctx *c, int world, const std::vector<int> &ranks) {
 // ---------------------------------------------------------------- transport
 enum Field { kU, kRhs, kV1, kV2 };
 
-static double *field(const PLevel &L, Field f) {
+static double *field(const PLevel &L, Field f, int buf = -1) {
     switch (f) {
-        case kU: return L.U();
+        case kU: return buf >= 0 ? L.F(L.u[buf]) : L.U();
         case kRhs: return L.F(L.rhs);
         case kV1: return L.F(L.v1);
         default: return L.F(L.v2);
@@ -197,14 +210,20 @@ static double *field(const PLevel &L, Field f) {
 struct XF {
     int l;
     Field f;
+    int buf = -1;   // kU: this u buffer instead of the current one
 };
 
-static int exchange_rows(mgx_ctx *c, std::initializer_list<XF> xs, hipStream_t st) {
+static int exchange_rows(mgx_ctx *c, const std::vector<XF> &xs, hipStream_t st) {
     Dist *d = c->dist;
     std::vector<Xfer> plan;
     if (d->local) {
         // part i's send to j lands where j's plan receives from i (the plan is
-        // checked pairwise at context creation: plan_check)
+        // checked pairwise at context creation: plan_check).  On the side
+        // stream the copies go to the DMA engines (no compute units), as an
+        // interconnect transfer would: as blit kernels beside the level passes
+        // they took CUs from them (level 1 +10 % at G=8)
+        const hipMemcpyKind kind =
+            st == d->xs ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToDevice;
         for (const XF &x : xs)
             for (size_t i = 0; i < d->parts.size(); ++i) {
                 const PLevel &L = d->parts[i].lv[x.l];
@@ -212,10 +231,10 @@ static int exchange_rows(mgx_ctx *c, std::initializer_list<XF> xs, hipStream_t s
                 ghost_plan(c->N, x.l, d->world, d->parts[i].rank, plan);
                 for (const Xfer &t : plan) {
                     PLevel &R = d->parts[t.peer].lv[x.l];
-                    HIPCHK(hipMemcpyAsync(field(R, x.f) + (long)t.send_row * P,
-                                          field(L, x.f) + (long)t.send_row * P,
-                                          sizeof(double) * (size_t)t.send_rows * P,
-                                          hipMemcpyDeviceToDevice, st));
+                    HIPCHK(hipMemcpyAsync(field(R, x.f, x.buf) + (long)t.send_row * P,
+                                          field(L, x.f, x.buf) + (long)t.send_row * P,
+                                          sizeof(double) * (size_t)t.send_rows * P, kind,
+                                          st));
                 }
             }
         return MGX_OK;
@@ -225,7 +244,7 @@ static int exchange_rows(mgx_ctx *c, std::initializer_list<XF> xs, hipStream_t s
     for (const XF &x : xs) {
         PLevel &L = p.lv[x.l];
         const long P = L.pitch;
-        double *a = field(L, x.f);
+        double *a = field(L, x.f, x.buf);
         ghost_plan(c->N, x.l, d->world, p.rank, plan);
         for (const Xfer &t : plan) {
             if (r != ncclSuccess) break;
@@ -245,7 +264,7 @@ static int exchange_rows(mgx_ctx *c, std::initializer_list<XF> xs, hipStream_t s
 
 // bytes moved by the parts this process holds: every row sent is read once
 // and written once
-static double halo_bytes(mgx_ctx *c, std::initializer_list<XF> xs) {
+static double halo_bytes(mgx_ctx *c, const std::vector<XF> &xs) {
     double bytes = 0;
     std::vector<Xfer> plan;
     for (const XF &x : xs)
@@ -256,7 +275,7 @@ static double halo_bytes(mgx_ctx *c, std::initializer_list<XF> xs) {
     return bytes;
 }
 
-static int exchange(mgx_ctx *c, std::initializer_list<XF> xs) {
+static int xchg(mgx_ctx *c, const std::vector<XF> &xs) {
     if (c->dist->world == 1 || xs.size() == 0) return MGX_OK;
     int rc = MGX_OK;
     CHK(launch(c, MGX_K_HALO, xs.begin()->l, halo_bytes(c, xs),
@@ -264,7 +283,59 @@ static int exchange(mgx_ctx *c, std::initializer_list<XF> xs) {
     return rc;
 }
 
-static int exchange(mgx_ctx *c, int l, Field f) { return exchange(c, {XF{l, f}}); }
+static int xchg(mgx_ctx *c, int l, Field f) { return xchg(c, std::vector<XF>{XF{l, f}}); }
+
+// The side stream's work is joined into the compute stream (dist_overlap).
+static int settle(mgx_ctx *c) {
+    Dist *d = c->dist;
+    if (!d->early_pending) return MGX_OK;
+    HIPCHK(hipStreamWaitEvent(c->stream, d->ev_join, 0));
+    d->early_pending = false;
+    return MGX_OK;
+}
+
+// Records the side stream's exchange like a launch (launch() times c->stream).
+template <class F>
+static int side_exchange(mgx_ctx *c, const std::vector<XF> &xs, F &&post) {
+    Dist *d = c->dist;
+    HIPCHK(hipEventRecord(d->ev_fork, c->stream));
+    HIPCHK(hipStreamWaitEvent(d->xs, d->ev_fork, 0));
+    const bool rec = c->prof == 1 || c->prof == 2;
+    hipEvent_t e0 = rec ? take_event(c) : nullptr, e1 = rec ? take_event(c) : nullptr;
+    if (e0) HIPCHK(hipEventRecord(e0, d->xs));
+    CHK(exchange_rows(c, xs, d->xs));
+    if (e0 && e1) {
+        HIPCHK(hipEventRecord(e1, d->xs));
+        const double b = halo_bytes(c, xs);
+        c->pending.push_back({MGX_K_HALO, 0, b, b, e0, e1});
+    }
+    HIPCHK(hipEventRecord(d->ev_join, d->xs));
+    post();
+    return MGX_OK;
+}
+
+// dist_overlap: the level-0 u ghost rows of buffer b (just written, next read
+// by a level-0 pass after the coarse levels) exchanged on the side stream now.
+static int early_u0(mgx_ctx *c, int b) {
+    Dist *d = c->dist;
+    if (g_dist_overlap == 0 || d->world == 1 || d->la < 1) return MGX_OK;
+    CHK(settle(c));
+    return side_exchange(c, {XF{0, kU, b}}, [&] {
+        d->early_pending = true;
+        d->early_buf = b;
+    });
+}
+
+// Whether the current level-0 u buffer's ghost rows are already exchanged
+// (early_u0); joins the side stream.  Consumes the state.
+static int take_fresh(mgx_ctx *c, bool *fresh) {
+    Dist *d = c->dist;
+    CHK(settle(c));
+    *fresh = d->early_buf >= 0 && !d->parts.empty() && !d->parts[0].lv.empty() &&
+             d->early_buf == d->parts[0].lv[0].cur;
+    d->early_buf = -1;
+    return MGX_OK;
+}
 
 // Restricted rhs of the first replicated level: every rank wrote its own rows
 // of the full array in its sub-context; make them whole everywhere.
@@ -342,6 +413,8 @@ static int smooth(mgx_ctx *c, int l, bool prolong, bool restrict_, bool norm) {
     Dist *d = c->dist;
     const int sweeps = c->opt.nsmooth;
     const int fuse = std::max(1, std::min(c->opt.fuse, mgx::kSmoothMaxSweeps));
+    bool fresh = false;   // level 0: u ghosts exchanged early (dist_overlap)
+    if (l == 0) CHK(take_fresh(c, &fresh));
     for (int done = 0; done < sweeps;) {
         const int k = std::min(sweeps - done, fuse);
         const bool first = done == 0, last = done + k == sweeps;
@@ -349,10 +422,11 @@ static int smooth(mgx_ctx *c, int l, bool prolong, bool restrict_, bool norm) {
         const bool pr = prolong && first && !zero;
         const bool rs = restrict_ && last;
         const bool nm = norm && last && !rs;
+        const bool ufresh = fresh && first;
         if (!zero && pr && l + 1 < d->la)
-            CHK(exchange(c, {XF{l, kU}, XF{l + 1, kU}}));
-        else if (!zero)
-            CHK(exchange(c, l, kU));
+            CHK(ufresh ? xchg(c, l + 1, kU) : xchg(c, {XF{l, kU}, XF{l + 1, kU}}));
+        else if (!zero && !ufresh)
+            CHK(xchg(c, l, kU));
         int mode = 0;
         if (zero) mode |= mgx::kModeZero;
         if (pr) mode |= mgx::kModeProlong;
@@ -403,7 +477,7 @@ static int smooth(mgx_ctx *c, int l, bool prolong, bool restrict_, bool norm) {
 static int coarse_rhs_ready(mgx_ctx *c, int l) {
     Dist *d = c->dist;
     if (l + 1 < d->la) {
-        CHK(exchange(c, l + 1, kRhs));
+        CHK(xchg(c, l + 1, kRhs));
         for (auto &p : d->parts) p.lv[l + 1].zero = true;
         return MGX_OK;
     }
@@ -448,39 +522,32 @@ static void dist_drop_spec(mgx_ctx *c) {
 // ghosts for the prolongation; afterwards the restricted rhs of the next cycle
 // is made ready on level 1 and the per-rank norm sums are reduced by the caller.
 //
-// dist_overlap = 1: the exchange goes on the second stream (forked after the
-// work that produced the sent rows) while the compute stream runs the pass's
-// unguarded interior march over rows [ra+16, rb-16) -- whose cone [ra+2, rb-2)
-// and coarse parents are all owned, so it needs no ghost row -- and the pass's
-// edge launch, which the split pass always has (boundary strips, global
-// bands), takes the two 16-row bands next to the ghosts too, after the join
-// (launch_xsmooth phases 1 and 2: no launch more than the plain pass).
+// dist_overlap >= 1: the level-0 ghosts were exchanged on the side stream
+// right after the pass that wrote them (early_u0), behind the coarse levels;
+// only level 1's u ghosts remain.  dist_overlap = 2: those go on the second
+// stream too (forked after the work that produced the sent rows) while the
+// compute stream runs the pass's unguarded interior march over rows
+// [ra+16, rb-16) -- whose cone [ra+2, rb-2) and coarse parents are all owned,
+// so it needs no ghost row -- and the pass's edge launch, which the split pass
+// always has (boundary strips, global bands), takes the two 16-row bands next
+// to the ghosts too, after the join (launch_xsmooth phases 1 and 2).
 // Outputs, u_pre / u_post / coarse rhs, are the same rows either way: bitwise.
 static int dist_cross(mgx_ctx *c, bool store_post) {
     Dist *d = c->dist;
     const int G = kGhostFine;
     const int k = c->opt.nsmooth;
-    bool ov = g_dist_overlap != 0 && d->world > 1;
+    // u ghosts of level 0 (unless exchanged early, dist_overlap) and of level 1
+    bool fresh = false;
+    CHK(take_fresh(c, &fresh));
+    std::vector<XF> xl;
+    if (!fresh) xl.push_back(XF{0, kU});
+    if (1 < d->la) xl.push_back(XF{1, kU});
+    bool ov = g_dist_overlap == 2 && d->world > 1 && !xl.empty();
     for (auto &p : d->parts) ov = ov && p.lv[0].rb - p.lv[0].ra >= 4 * G && p.lv[0].coef.dgs > 0;
-    auto xs = {XF{0, kU}, XF{1, kU}};
-    auto x0 = {XF{0, kU}};
-    if (ov) {
-        HIPCHK(hipEventRecord(d->ev_fork, c->stream));
-        HIPCHK(hipStreamWaitEvent(d->xs, d->ev_fork, 0));
-        // profiled like a launch, on the side stream (launch() times c->stream)
-        const bool rec = c->prof == 1 || c->prof == 2;
-        hipEvent_t e0 = rec ? take_event(c) : nullptr, e1 = rec ? take_event(c) : nullptr;
-        if (e0) HIPCHK(hipEventRecord(e0, d->xs));
-        CHK(exchange_rows(c, 1 < d->la ? xs : x0, d->xs));
-        if (e0 && e1) {
-            HIPCHK(hipEventRecord(e1, d->xs));
-            const double b = halo_bytes(c, 1 < d->la ? xs : x0);
-            c->pending.push_back({MGX_K_HALO, 0, b, b, e0, e1});
-        }
-        HIPCHK(hipEventRecord(d->ev_join, d->xs));
-    } else {
-        CHK(exchange(c, 1 < d->la ? xs : x0));
-    }
+    if (ov)
+        CHK(side_exchange(c, xl, [] {}));
+    else if (!xl.empty())
+        CHK(xchg(c, xl));
     // one launch (phase 1 / 2) or both of the pass over owned rows [ra, rb) of part p
     auto pass = [&](Part &p, int P, int Q, int phase, int done) -> int {
         PLevel &L = p.lv[0];
@@ -581,7 +648,11 @@ static int dist_cross(mgx_ctx *c, bool store_post) {
         L.spec = bufs[i].second;
         L.zero = false;
     }
-    return coarse_rhs_ready(c, 0);
+    CHK(coarse_rhs_ready(c, 0));
+    // the next cycle's level-0 input is u_pre: its ghosts now, on the side
+    // stream, behind the coarse levels (after the coarse rhs exchange, which
+    // the next level needs first)
+    return early_u0(c, d->parts[0].lv[0].spec);
 }
 
 bool dist_post_predictable(mgx_ctx *c) {
@@ -625,6 +696,7 @@ int dist_vcycle(mgx_ctx *c, double *norm, bool store_post) {
         } else {
             CHK(smooth(c, 0, false, /*restrict=*/true, false));
             CHK(coarse_rhs_ready(c, 0));
+            CHK(early_u0(c, d->parts[0].lv[0].cur));
         }
         CHK(coarse_cycle(c, 1));
         if (c->post_only) {   // mg_outer's last cycle: post-smoothing + norm only
@@ -644,11 +716,12 @@ int dist_vcycle(mgx_ctx *c, double *norm, bool store_post) {
 int dist_residual_norm(mgx_ctx *c, double *norm) {
     Dist *d = c->dist;
     HIPCHK(hipSetDevice(c->device));
+    CHK(settle(c));
     if (d->la == 0) {
         for (auto &p : d->parts) CHK(op_residual_norm(p.sub, 0, norm));
         return MGX_OK;
     }
-    CHK(exchange(c, 0, kU));
+    CHK(xchg(c, 0, kU));
     for (auto &p : d->parts) {
         PLevel &L = p.lv[0];
         CHK(launch(c, MGX_K_RESNORM, 0, 48.0 * L.Mown(), 32.0 * L.Mown(), [&] {
@@ -663,12 +736,13 @@ int dist_residual_norm(mgx_ctx *c, double *norm) {
 int dist_rhs(mgx_ctx *c) {
     Dist *d = c->dist;
     HIPCHK(hipSetDevice(c->device));
+    CHK(settle(c));
     dist_drop_spec(c);
     if (d->la == 0) {
         for (auto &p : d->parts) CHK(op_rhs(p.sub));
         return MGX_OK;
     }
-    CHK(exchange(c, 0, kU));
+    CHK(xchg(c, 0, kU));
     for (auto &p : d->parts) {
         PLevel &L = p.lv[0];
         CHK(launch(c, MGX_K_RHS, 0, 32.0 * L.Mown(), [&] {
@@ -676,7 +750,7 @@ int dist_rhs(mgx_ctx *c) {
                             c->stream, L.ra, L.rb);
         }));
     }
-    return exchange(c, 0, kRhs);
+    return xchg(c, 0, kRhs);
 }
 
 // compute_rhs + the initial residual norm of mg_outer in one pass per part
@@ -684,12 +758,13 @@ int dist_rhs(mgx_ctx *c) {
 int dist_rhs_norm(mgx_ctx *c, double *res0) {
     Dist *d = c->dist;
     HIPCHK(hipSetDevice(c->device));
+    CHK(settle(c));
     dist_drop_spec(c);
     if (d->la == 0) {
         CHK(dist_rhs(c));
         return dist_residual_norm(c, res0);
     }
-    CHK(exchange(c, 0, kU));
+    CHK(xchg(c, 0, kU));
     for (auto &p : d->parts) {
         PLevel &L = p.lv[0];
         CHK(launch(c, MGX_K_RHS, 0, 80.0 * L.Mown(), 32.0 * L.Mown(), [&] {
@@ -698,7 +773,7 @@ int dist_rhs_norm(mgx_ctx *c, double *res0) {
                                  /*take_sqrt=*/false);
         }));
     }
-    CHK(exchange(c, 0, kRhs));
+    CHK(xchg(c, 0, kRhs));
     return reduce_norm(c, res0);
 }
 
@@ -743,6 +818,8 @@ int dist_upload(mgx_ctx *c, const double *u0, const double *v1, const double *v2
                 hipMemcpyKind kind) {
     Dist *d = c->dist;
     HIPCHK(hipSetDevice(c->device));
+    CHK(settle(c));
+    d->early_buf = -1;
     mgx_options o = c->opt;
     o.device = -1;
     mgx_ctx *T = nullptr;
@@ -797,6 +874,7 @@ int dist_upload(mgx_ctx *c, const double *u0, const double *v1, const double *v2
 int dist_download(mgx_ctx *c, double *u, hipMemcpyKind kind) {
     Dist *d = c->dist;
     HIPCHK(hipSetDevice(c->device));
+    CHK(settle(c));
     if (d->la == 0) {
         mgx_ctx *s = d->parts[0].sub;
         Level &L = s->lv[0];
@@ -865,6 +943,7 @@ int dist_owned_rows(mgx_ctx *c, int part, int *ra, int *rb) {
 int dist_download_rows(mgx_ctx *c, int part, double *out, hipMemcpyKind kind) {
     Dist *d = c->dist;
     HIPCHK(hipSetDevice(c->device));
+    CHK(settle(c));
     int ra, rb;
     CHK(dist_owned_rows(c, part, &ra, &rb));
     const long n = c->N;
@@ -898,6 +977,8 @@ static int dist_upload_rows_impl(mgx_ctx *c, const double *const *u0s,
                                  const double *const *v1s, const double *const *v2s) {
     Dist *d = c->dist;
     HIPCHK(hipSetDevice(c->device));
+    CHK(settle(c));
+    d->early_buf = -1;
     if (c->opt.tower_mode != MGX_TOWER_CORRECT)
         return fail(MGX_E_ARG, "mgx_upload_rows: needs tower_mode MGX_TOWER_CORRECT (the "
                                "reference tower mixes rows of the whole grid)");
@@ -947,7 +1028,7 @@ static int dist_upload_rows_impl(mgx_ctx *c, const double *const *u0s,
                 CHK(check_launch("tower injection (rows)"));
             }
         }
-        CHK(exchange(c, {XF{l, kV1}, XF{l, kV2}}));
+        CHK(xchg(c, {XF{l, kV1}, XF{l, kV2}}));
     }
     // first replicated level: owned rows into each sub-context, all-gathered
     const long nl = c->N >> d->la, q = nl / d->world;

@@ -111,6 +111,8 @@ int prof_flush(mgx_ctx *c) {
     HIPCHK(hipStreamSynchronize(c->stream));
     for (auto &r : c->pending) {
         float ms = 0.f;
+        // (a partitioned context times its side-stream exchanges too)
+        HIPCHK(hipEventSynchronize(r.e1));
         HIPCHK(hipEventElapsedTime(&ms, r.e0, r.e1));
         int lvl = r.level < 0 ? 0 : (r.level > 63 ? 63 : r.level);
         c->sum_ms[r.kind][lvl] += ms;
@@ -1347,7 +1349,7 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         return MGX_OK;
     }
     if (!strcmp(key, "dist_overlap")) {
-        if (value != 0 && value != 1) return fail(MGX_E_ARG, "dist_overlap must be 0 or 1");
+        if (value < 0 || value > 2) return fail(MGX_E_ARG, "dist_overlap must be 0, 1 or 2");
         mgxi::g_dist_overlap = value;
         return MGX_OK;
     }

@@ -110,7 +110,7 @@ def rccl_selfcheck(world: int, rank: int, device: int, n: int = 4096, maxlvl: in
     ok, err, la = True, 0.0, None
     try:
         _lib.set_tuning("dist_min_rows", 16)
-        for ov in (0, 1):
+        for ov in (0, 1, 2):
             _lib.set_tuning("dist_overlap", ov)
             uid = broadcast_unique_id(group)
             with Multigrid(n, maxlvl, dt, nu, device=device, world=world, rank=rank,
@@ -136,5 +136,5 @@ def rccl_selfcheck(world: int, rank: int, device: int, n: int = 4096, maxlvl: in
     dist.broadcast(verdict, src=0, group=group)
     ok, err = bool(verdict[0].item() == 1.0), float(verdict[1].item())
     return {"N": n, "levels": maxlvl, "cycles": cycles, "partitioned_levels": la,
-            "overlap": [0, 1], "bitwise": ok, "norm_rel_err": err,
+            "overlap": [0, 1, 2], "bitwise": ok, "norm_rel_err": err,
             "passed": ok and err <= 1e-11}

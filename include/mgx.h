@@ -168,10 +168,13 @@ int mgx_synchronize(mgx_ctx *ctx);
  * the next cycle's restricted rhs, not the last correction.  0 = off.
  * "dist_min_rows": partitioned solvers replicate every level whose row blocks
  * would be shorter than this (default 256, even, >= 16); read at creation.
- * "dist_overlap": 1 = on partitioned contexts the finest level's ghost
- * exchange runs on a second stream while the cross-cycle pass updates the
- * rows whose cone stays inside the block; the two 16-row bands next to the
- * ghosts follow the exchange (default 0; bitwise the same results).
+ * "dist_overlap": partitioned contexts, 1 = the finest level's u
+ * ghost rows are exchanged on a second stream as soon as the pass that wrote
+ * them ends, hidden behind the coarse levels (the next finest pass waits for
+ * it); 2 = that, and the cross pass's remaining exchange (level-1 u) on the
+ * second stream beside the pass's interior march, the two 16-row bands next
+ * to the ghosts after it; 0 (default) = every exchange on the compute stream.
+ * Bitwise the same results.
  * "xfast": 1 (default) runs the cross-cycle pass as an unguarded kernel over
  * the interior strips and rows plus a guarded kernel over the boundary strips
  * and bands; 0 = one guarded launch (bitwise the same results).

@@ -134,6 +134,8 @@ struct ncclComm {
     int rank = 0, world = 0;
     long seq = 0;                      // collectives issued by this rank
     std::vector<hipEvent_t> events;    // destroyed with the communicator
+    double *stage = nullptr;           // all-reduce staging (this rank's stream only)
+    size_t stage_bytes = 0;
     hipEvent_t event() {
         hipEvent_t e = nullptr;
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
@@ -329,8 +331,19 @@ ncclResult_t collective(CollKind kind, const void *send, void *recv, size_t coun
         } else if (kind == kCollBroadcast) {
             if (me != root || send != recv) cp(recv, c->send[root], bytes, root);
         } else {
-            if (hipMallocAsync((void **)&stage, bytes * R, st) != hipSuccess)
-                rc = bad(ncclUnhandledCudaError, "staging alloc");
+            // a persistent per-rank staging buffer, used in this rank's stream
+            // order only (grown, with a device sync, for a larger count)
+            if (comm->stage_bytes < bytes * R) {
+                (void)hipDeviceSynchronize();
+                (void)hipFree(comm->stage);
+                comm->stage = nullptr;
+                comm->stage_bytes = 0;
+                if (hipMalloc((void **)&comm->stage, bytes * R) == hipSuccess)
+                    comm->stage_bytes = bytes * R;
+                else
+                    rc = bad(ncclUnhandledCudaError, "staging alloc");
+            }
+            stage = comm->stage;
             for (int r = 0; rc == ncclSuccess && r < R; ++r)
                 cp(reinterpret_cast<char *>(stage) + (size_t)r * bytes, c->send[r], bytes, r);
         }
@@ -348,14 +361,11 @@ ncclResult_t collective(CollKind kind, const void *send, void *recv, size_t coun
         if (r != me && hipStreamWaitEvent(st, c->read_done[r], 0) != hipSuccess)
             rc = bad(ncclUnhandledCudaError, "stream wait");
     // (4)
-    if (kind == kCollAllReduce && stage) {
-        if (rc == ncclSuccess) {
-            const unsigned blocks = (unsigned)((count + 255) / 256);
-            hipLaunchKernelGGL(k_sum_ranks, dim3(blocks ? blocks : 1), dim3(256), 0, st,
-                               static_cast<double *>(recv), stage, count, R);
-            if (hipGetLastError() != hipSuccess) rc = bad(ncclUnhandledCudaError, "sum kernel");
-        }
-        (void)hipFreeAsync(stage, st);
+    if (kind == kCollAllReduce && stage && rc == ncclSuccess) {
+        const unsigned blocks = (unsigned)((count + 255) / 256);
+        hipLaunchKernelGGL(k_sum_ranks, dim3(blocks ? blocks : 1), dim3(256), 0, st,
+                           static_cast<double *>(recv), stage, count, R);
+        if (hipGetLastError() != hipSuccess) rc = bad(ncclUnhandledCudaError, "sum kernel");
     }
     {
         std::lock_guard<std::mutex> g(q.mu);
@@ -413,11 +423,27 @@ ncclResult_t ncclCommInitRank(ncclComm_t *out, int nranks, ncclUniqueId id, int 
     q->alive++;
     q->cv.notify_all();
     q->cv.wait(g, [&] { return q->joined == q->world; });   // init is collective
+    g.unlock();
     ncclComm_t c = new ncclComm();
     c->q = q;
     c->key = key;
     c->rank = rank;
     c->world = nranks;
+    if (hipMalloc((void **)&c->stage, 1 << 16) != hipSuccess)
+        return bad(ncclUnhandledCudaError, "staging alloc");
+    c->stage_bytes = 1 << 16;
+    {   // load the sum kernel once, outside any concurrent launch
+        static std::mutex warm_mu;
+        static bool warm = false;
+        std::lock_guard<std::mutex> w(warm_mu);
+        if (!warm) {
+            hipLaunchKernelGGL(k_sum_ranks, dim3(1), dim3(256), 0, nullptr, c->stage, c->stage,
+                               (size_t)0, 1);
+            if (hipDeviceSynchronize() != hipSuccess)
+                return bad(ncclUnhandledCudaError, "sum kernel warm-up");
+            warm = true;
+        }
+    }
     *out = c;
     return ncclSuccess;
 }
@@ -429,6 +455,7 @@ ncclResult_t ncclCommDestroy(ncclComm_t c) {
         (void)hipEventSynchronize(e);
         (void)hipEventDestroy(e);
     }
+    (void)hipFree(c->stage);
     bool last;
     {
         std::lock_guard<std::mutex> g(c->q->mu);

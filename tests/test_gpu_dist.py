@@ -312,18 +312,19 @@ def overlap():
 
 @pytest.mark.parametrize("G", [2, 4, 8])
 def test_overlapped_exchange_bitwise(G, overlap):
-    """dist_overlap = 1 (finest ghost exchange on a second stream beside the
-    interior of the cross pass, then the two ghost bands) gives the same u
-    bitwise as the serialised schedule and as one GPU, norms to the
-    summation-order tolerance (the split pass adds three partial sums)."""
+    """dist_overlap = 1 (finest ghost rows exchanged on a second stream behind
+    the coarse levels) and 2 (plus the level-1 exchange beside the interior of
+    the cross pass, the two ghost bands after it) give the same u bitwise as
+    the serialised schedule and as one GPU, norms to the summation-order
+    tolerance (the split pass sums its partials in another order)."""
     N, L = 4096, 7
     dt = 1.0 / N / 10
     us, ns, rs, _ = _run(N, L, dt, NU, 4)
     out = {}
-    for ov in (0, 1):
+    for ov in (0, 1, 2):
         overlap(ov)
         out[ov] = _run(N, L, dt, NU, 4, parts=G)
-    for ov in (0, 1):
+    for ov in (0, 1, 2):
         up, npart, rp, info = out[ov]
         assert info[0] == G
         assert np.array_equal(up, us), ov

@@ -33,7 +33,7 @@ def _scenarios():
     # N=4096: the cross-cycle pass on row blocks, levels 0..5 partitioned at
     # world 8; exchanges on the compute stream and overlapped
     for G in (2, 4, 8):
-        for ov in (0, 1):
+        for ov in (0, 1, 2):
             sc.append(dict(N=4096, L=7, world=G, min_rows=16, overlap=ov, full_download=True))
     # row-block upload (the C5 path: correct tower built from the blocks)
     sc.append(dict(N=4096, L=7, world=4, min_rows=16, overlap=1, row_upload=True,
@@ -42,6 +42,7 @@ def _scenarios():
     sc.append(dict(N=16384, L=9, world=2, overlap=1))
     sc.append(dict(N=16384, L=9, world=8, overlap=0))
     sc.append(dict(N=16384, L=9, world=8, overlap=1))
+    sc.append(dict(N=16384, L=9, world=8, overlap=2))
     return sc
 
 
