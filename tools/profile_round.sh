@@ -11,7 +11,7 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
-    -- python3 bench.py --steps 10 --warmup 2 --cpu-baseline off > "$OUT/bench_prof.log" 2>&1
+    -- python3 bench.py --steps 10 --warmup 2 --cpu-baseline off --no-generic > "$OUT/bench_prof.log" 2>&1
 grep '^{' "$OUT/bench_prof.log" | tail -1 > "$OUT/bench.json"
 cp "$(find "$OUT/trace" -name 'run_kernel_stats.csv' | head -1)" "$OUT/kernel_stats.csv"
 # same cycle pattern as the bench: one run_cycles(10) call
