@@ -1071,6 +1071,10 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
 #ifndef MGX_XACOEF
 #define MGX_XACOEF 1
 #endif
+// fewest rows per workgroup of the guarded edge launch
+#ifndef MGX_XEDGE_ROWS
+#define MGX_XEDGE_ROWS 16
+#endif
 template <int K>
 struct XCfg {
     static constexpr int S = 2 * K;
@@ -1144,8 +1148,10 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     // u 3-4 steps or rhs/v 5 measured no better (N=16384, tools/ab_libs.sh).
     constexpr int XRV = MGX_XRV;
     constexpr int XU = MGX_XU;
-    // A forms each row's coefficients once (MGX_XACOEF; B always does)
-    constexpr bool XACOEF = MGX_XACOEF != 0;
+    // A forms each row's coefficients once (MGX_XACOEF; B always does).  Not
+    // in the guarded edge kernel: there it takes the kernel past 256 VGPRs
+    // (one wave per SIMD), and the edge launch is latency bound
+    constexpr bool XACOEF = MGX_XACOEF != 0 && !G;
     static_assert(XU >= 1 && XU <= NR - 3, "u prefetch distance");
     // row s+XRV takes the ring slot of row s+XRV-NR, last used by A's norm of
     // row s+1-S
@@ -2662,7 +2668,8 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
                                                                 kNormBlocks / (2 * WPB) / 2, s);
     if (A.phase == 1) return pm;
     const int pe = xsmooth_launch<1, K, true>(A, edge, A.partials + pm, lo, hi,
-                                              std::min(32, A.min_rows), kNormBlocks / 2 / 2, s);
+                                              std::min(MGX_XEDGE_ROWS, A.min_rows),
+                                              kNormBlocks / 2 / 2, s);
     return pm + pe;
 }
 
