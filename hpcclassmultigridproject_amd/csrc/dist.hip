@@ -42,12 +42,13 @@ long g_dist_min_rows = 256;
 // for it); 2 = that, and the cross pass's remaining exchange (level-1 u) on
 // the second stream too, beside the pass's interior march (the bands next to
 // the ghosts go to its edge launch); 0 (default) = every exchange on the
-// compute stream.  On virtual ranks (one GPU) the early exchange's copies
-// compete with the level passes for the same chip and cost 2-3 %; over xGMI
-// it takes the level-0 exchange (2 x 16 rows, ~4 MB per rank) off the critical
-// path -- bench.py prices 0 / 1 / 2 on the N-GPU run itself and keeps the
-// fastest for its timed region
-long g_dist_overlap = 0;
+// compute stream; -1 (default) = 1 on an RCCL communicator, 0 on virtual
+// ranks.  On virtual ranks (one GPU) the early exchange's copies compete with
+// the level passes for the same chip and cost 2-3 %; over xGMI it takes the
+// level-0 exchange (2 x 16 rows, ~4 MB per rank) off the critical path for
+// nothing of the local HBM -- bench.py prices 0 / 1 / 2 on the N-GPU run
+// itself and keeps the fastest for its timed region
+long g_dist_overlap = -1;
 
 // the partition / exchange plan (plan.h, host-only)
 using mgxplan::alloc_rows;
@@ -120,6 +121,12 @@ struct Dist {
     int early_buf = -1;
     bool early_pending = false;
 };
+
+// the effective dist_overlap of a context (-1: by transport)
+static long overlap_mode(const Dist *d) {
+    if (g_dist_overlap >= 0) return g_dist_overlap;
+    return d->comm ? 1 : 0;
+}
 
 void dist_free(mgx_ctx *c) {
     Dist *d = c->dist;
@@ -318,7 +325,7 @@ static int side_exchange(mgx_ctx *c, const std::vector<XF> &xs, F &&post) {
 // by a level-0 pass after the coarse levels) exchanged on the side stream now.
 static int early_u0(mgx_ctx *c, int b) {
     Dist *d = c->dist;
-    if (g_dist_overlap == 0 || d->world == 1 || d->la < 1) return MGX_OK;
+    if (overlap_mode(d) == 0 || d->world == 1 || d->la < 1) return MGX_OK;
     CHK(settle(c));
     return side_exchange(c, {XF{0, kU, b}}, [&] {
         d->early_pending = true;
@@ -542,7 +549,7 @@ static int dist_cross(mgx_ctx *c, bool store_post) {
     std::vector<XF> xl;
     if (!fresh) xl.push_back(XF{0, kU});
     if (1 < d->la) xl.push_back(XF{1, kU});
-    bool ov = g_dist_overlap == 2 && d->world > 1 && !xl.empty();
+    bool ov = overlap_mode(d) == 2 && d->world > 1 && !xl.empty();
     for (auto &p : d->parts) ov = ov && p.lv[0].rb - p.lv[0].ra >= 4 * G && p.lv[0].coef.dgs > 0;
     if (ov)
         CHK(side_exchange(c, xl, [] {}));

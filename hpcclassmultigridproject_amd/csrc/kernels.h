@@ -139,6 +139,8 @@ bool xstep_supported(long n);
 // Cross pass: 1 = interior strips run the unguarded march (default), 0 = all guarded.
 void set_xfast(long v);
 long get_xfast();
+void set_march_tile_rows(long v);
+long get_march_tile_rows();
 // Cross pass on row blocks of <= xtile_max_rows rows (default 4097): edges as
 // LDS tiles instead of the guarded march (0 = never).
 void set_xtile_max_rows(long v);

@@ -935,7 +935,8 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                     const int iS = (p + 2 - h + 2 * NR) % NR;
                     const int cs = ((p + 1 - h) & 1) ^ (h & 1);
                     const RowData &d = rd[iR];
-                    const bool inr = !G || (r >= 1 && r <= n - 1);
+                    // (one unsigned compare: r in [1, n-1])
+                    const bool inr = !G || (unsigned)(r - 1) < (unsigned)(n - 1);
                     // unguarded: fresh scalar nu per stage (no cross-stage
                     // coefficient CSE: it would need more VGPRs, see k_xsmooth)
                     Coef cg = c;
@@ -2706,7 +2707,10 @@ long get_tile_max_n();
 static long tile_max_n() {
     if (g_tile_max_n < 0) {
         const char *e = getenv("MGX_TILE_MAX_N");
-        g_tile_max_n = e ? atol(e) : 2048;
+        // 1024: level 3 (n = 2048) as a wave march, 0.115 -> 0.105-0.110 ms
+        // per cycle at N=16384 (tools/ab_levels.py); levels 4-5 measure the
+        // same either way
+        g_tile_max_n = e ? atol(e) : 1024;
     }
     return g_tile_max_n;
 }
@@ -2758,6 +2762,14 @@ static int smooth_tile_inst(const SmoothArgs &A, hipStream_t s) {
     return smooth_tile_rows<K, MODE, 16>(A, s);
 }
 
+// a row block runs as LDS tiles when its march would give the resident waves
+// fewer than this many rows each (tuning key "march_tile_rows"; 16: level 2
+// on 4 row blocks marches, 0.50 -> 0.46 ms for the 4 parts; level 1 on 8 row
+// blocks as tiles (64, 96) costs +25-45 %)
+long g_march_tile_rows = 16;
+void set_march_tile_rows(long v) { g_march_tile_rows = v; }
+long get_march_tile_rows() { return g_march_tile_rows; }
+
 template <int K, int MODE>
 static int smooth_block(const SmoothArgs &A, hipStream_t s) {
     // the row march needs >= ~32 rows per wave to amortise its priming rows;
@@ -2776,7 +2788,7 @@ static int smooth_block(const SmoothArgs &A, hipStream_t s) {
             slots = std::max(1, cus) * std::max(1, per);
         }
         const long groups = (A.n + 1 + W4 - 1) / W4;
-        tile = groups * (A.rb - A.ra) < (long)slots * 32;
+        tile = groups * (A.rb - A.ra) < (long)slots * g_march_tile_rows;
     }
     if (tile) {
         const int g = smooth_tile_inst<K, MODE>(A, s);

@@ -1349,7 +1349,7 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         return MGX_OK;
     }
     if (!strcmp(key, "dist_overlap")) {
-        if (value < 0 || value > 2) return fail(MGX_E_ARG, "dist_overlap must be 0, 1 or 2");
+        if (value < -1 || value > 2) return fail(MGX_E_ARG, "dist_overlap must be -1, 0, 1 or 2");
         mgxi::g_dist_overlap = value;
         return MGX_OK;
     }
@@ -1428,6 +1428,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgxi::g_zero_rows = value;
         return MGX_OK;
     }
+    if (!strcmp(key, "march_tile_rows")) {
+        if (value < 0) return fail(MGX_E_ARG, "march_tile_rows must be >= 0");
+        mgx::set_march_tile_rows(value);
+        return MGX_OK;
+    }
     return fail(MGX_E_ARG, std::string("mgx_set_tuning: unknown key ") + key);
 }
 extern "C" int mgx_get_tuning(const char *key, long *value) {
@@ -1503,6 +1508,10 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "zero_rows")) {
         *value = mgxi::g_zero_rows;
+        return MGX_OK;
+    }
+    if (!strcmp(key, "march_tile_rows")) {
+        *value = mgx::get_march_tile_rows();
         return MGX_OK;
     }
     return fail(MGX_E_ARG, std::string("mgx_get_tuning: unknown key ") + key);

@@ -159,7 +159,7 @@ int mgx_stream(mgx_ctx *ctx, void **stream);
 int mgx_synchronize(mgx_ctx *ctx);
 
 /* Process-wide tuning knobs.  "tile_max_n": levels with n <= value run the
- * fused smoothing pass as 2-D LDS tiles instead of the row march (default 2048;
+ * fused smoothing pass as 2-D LDS tiles instead of the row march (default 1024;
  * env MGX_TILE_MAX_N).
  * "cross_cycle": 1 (default) fuses, inside mg_outer / run_cycles / step, the
  * finest level's post-smoothing of each V-cycle with the pre-smoothing of
@@ -173,11 +173,14 @@ int mgx_synchronize(mgx_ctx *ctx);
  * them ends, hidden behind the coarse levels (the next finest pass waits for
  * it); 2 = that, and the cross pass's remaining exchange (level-1 u) on the
  * second stream beside the pass's interior march, the two 16-row bands next
- * to the ghosts after it; 0 (default) = every exchange on the compute stream.
- * Bitwise the same results.
+ * to the ghosts after it; 0 = every exchange on the compute stream; -1
+ * (default) = 1 on an RCCL communicator, 0 on virtual ranks (one GPU, where
+ * the side stream's copies compete with the passes).  Bitwise the same results.
  * "xfast": 1 (default) runs the cross-cycle pass as an unguarded kernel over
  * the interior strips and rows plus a guarded kernel over the boundary strips
  * and bands; 0 = one guarded launch (bitwise the same results).
+ * "march_tile_rows": a row block whose wave march would give each resident
+ * workgroup fewer than this many rows runs as LDS tiles (default 16, >= 0).
  * "xtile_max_rows": on row blocks of at most this many rows (a rank of a
  * partitioned solver, a small level) the cross-cycle pass runs the boundary
  * strips and bands as LDS tiles instead of the guarded row march (latency

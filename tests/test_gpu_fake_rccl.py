@@ -40,6 +40,8 @@ def _scenarios():
                    full_download=True))
     # the headline size, default partition (levels 0..5 split at world 8)
     sc.append(dict(N=16384, L=9, world=2, overlap=1))
+    # the default (-1): overlapped on an RCCL communicator
+    sc.append(dict(N=4096, L=7, world=4, min_rows=16, overlap=-1))
     sc.append(dict(N=16384, L=9, world=8, overlap=0))
     sc.append(dict(N=16384, L=9, world=8, overlap=1))
     sc.append(dict(N=16384, L=9, world=8, overlap=2))
