@@ -139,6 +139,11 @@ bool xstep_supported(long n);
 // Cross pass: 1 = interior strips run the unguarded march (default), 0 = all guarded.
 void set_xfast(long v);
 long get_xfast();
+// Cross pass interior kernel: 1 = the group-exchange form (a workgroup's strips
+// adjacent, edge columns through LDS: 28 halo columns per 512), 0 = separate
+// strips with their own halos (28 per 128).  Bitwise the same.
+void set_xgroup(long v);
+long get_xgroup();
 void set_march_tile_rows(long v);
 long get_march_tile_rows();
 // Cross pass on row blocks of <= xtile_max_rows rows (default 4097): edges as

@@ -679,6 +679,22 @@ __device__ __forceinline__ double dpp_shl1(double v) {
     const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), 0x130, 0xf, 0xf, true);
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
+// the same shifts, the edge lane (0 / 63) keeping `old` (bound_ctrl off:
+// its write is disabled, so the v_mov_b32_dpp leaves the old value in place)
+__device__ __forceinline__ double dpp_shr1_or(double v, double old) {
+    const long long b = __double_as_longlong(v), o = __double_as_longlong(old);
+    const int lo = __builtin_amdgcn_update_dpp((int)o, (int)b, 0x138, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), 0x138, 0xf, 0xf,
+                                               false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double dpp_shl1_or(double v, double old) {
+    const long long b = __double_as_longlong(v), o = __double_as_longlong(old);
+    const int lo = __builtin_amdgcn_update_dpp((int)o, (int)b, 0x130, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), 0x130, 0xf, 0xf,
+                                               false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
 // gs.cpp:130 / :75 with the velocity terms pre-scaled: t1 = v1*h/2, t2 = v2*h/2
 template <bool POSD = false>
 __device__ __forceinline__ double gs_point_t(double rhs, double t1, double t2, double uN,
@@ -1129,7 +1145,32 @@ struct XCfg {
 // fl(sa[R] * fl(sb[c]*h/2)) -- bitwise fl(v*h/2), the scalings by h/2 being
 // exact (sepvel.h checks the range) -- from the lane's column factors, held
 // in registers for the whole march.
-template <int WPB, int K, bool G, bool RS = false, bool SV = false>
+//
+// XG = true (group exchange, unguarded only): the WPB pairs of a workgroup
+// march WPB ADJACENT 128-column strips that overlap by nothing, and the
+// workgroup as a whole is one 64*WPB-lane strip with the H-pair halo only on
+// its two outer sides: group g owns WGc = 128*WPB - 4H columns (484 instead of
+// 4 x 100).  The columns a wave's edge lanes need from the neighbouring wave
+// of the same role (lane 0 the west wave's column c0-1, lane 63 the east
+// wave's column c0+2) come through LDS: all inputs of a march step's stages
+// and residuals from a neighbouring column are results of the PREVIOUS step
+// (a stage on row r updates one colour; the other colour of row r was last
+// updated by the stage before, one step earlier, or is the row's initial
+// value), so each wave posts, at the end of a step, lane 0's .x and lane 63's
+// .y of every row it changed (and of the row that entered its ring), and a
+// barrier per step (instead of per two steps) orders post and use.  The
+// edge lane takes the posted value through the DPP shift's "keep old" form
+// (bound_ctrl off): no extra VALU instruction.  The halo work of the pass
+// drops from 28 of 128 columns to 28 of 512.
+#ifndef MGX_XG_DBG
+#define MGX_XG_DBG 0
+#endif
+struct XGeo {
+    int x0, xl, xend, glast;   // XG: owned origin of group 0, origin of the last group, end
+    int ec0, ec1, er0, er1;    // guarded kernel: [ec0, ec1) x [er0, er1) owned by the XG launch
+};
+
+template <int WPB, int K, bool G, bool RS = false, bool SV = false, bool XG = false>
 __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     const double *__restrict__ uin, double *__restrict__ upost, double *__restrict__ upre,
     const double *__restrict__ rhs, const double *__restrict__ v1, const double *__restrict__ v2,
@@ -1138,10 +1179,12 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     int lo, int hi, int store_post, double *__restrict__ rhs_next,
     double *__restrict__ partials2, const double *__restrict__ sa1,
     const double *__restrict__ sb1, const double *__restrict__ sa2,
-    const double *__restrict__ sb2) {
+    const double *__restrict__ sb2, XGeo xg) {
     using X = XCfg<K>;
     constexpr int S = X::S, H = X::H, NR = X::NR, W = X::W, D = X::D, NU = X::NU,
                   NRD = X::NRD, EA = X::EA, EB = X::EB;
+    static_assert(!XG || !G, "the group exchange is the unguarded kernel's");
+    constexpr int WGc = 128 * WPB - 4 * H;
     // A's prefetch distances in steps: rhs/v rows XRV ahead of their first
     // stage, u rows (+ coarse parents) XU ahead of entering the ring.  The
     // pass is bound by loads in flight, not by VALU: rhs/v 2 -> 3 -> 4 steps
@@ -1160,6 +1203,13 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     __shared__ double2 uring[WPB][NU][64];
     // rhs / t1 / t2 planes: each hand-off access is 16 B per lane, unit stride
     __shared__ double2 rdring[WPB][NRD][3][64];
+    // XG: per role and wave, lane 0's .x (xchx) and lane 63's .y (xchy) of
+    // each ring row, slot = row mod NR (the register rings' index)
+    // (entries 0 and WPB+1 of each role: the outer waves' outer neighbours,
+    // never written -- read only by halo lanes -- so that a wave's own, west
+    // and east entries sit at fixed offsets from one address)
+    __shared__ double xchx[XG ? 2 : 1][XG ? WPB + 2 : 1][XG ? NR : 1],
+        xchy[XG ? 2 : 1][XG ? WPB + 2 : 1][XG ? NR : 1];
 
     const int l = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
@@ -1171,13 +1221,56 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     const double hh = c.h * 0.5;
     double acc = 0.0, acc2 = 0.0;
 
-    // One march of the pair over owned rows [a, b) of strip j0 (G: see above;
-    // the unguarded form keeps only the uniform owned-row tests of its outputs)
-    auto march = [&](const int j0, const int a, const int b) {
+    // One march of the pair over owned rows [a, b) of the strip whose lane 0
+    // is column cb, owning columns [k0, k1) (G: see above; the unguarded form
+    // keeps only the uniform owned-row tests of its outputs)
+    auto march = [&](const int cb, const int k0, const int k1, const int a, const int b) {
         constexpr bool GM = G, GS = G, GN = G;   // make_u / stage / residual guards
-        const int c0 = j0 - 2 * H + 2 * l;
+        const int c0 = cb + 2 * l;
         const bool act = c0 >= 0 && c0 <= n;
-        const bool keep = act && l >= H && l < 64 - H;
+        // the guarded kernel beside an XG launch: rows [er0, er1) of columns
+        // [ec0, ec1) are that launch's (one owner per output)
+        const bool exc = G && c0 >= xg.ec0 && c0 < xg.ec1;
+        const bool keep = act && c0 >= k0 && c0 < k1;
+        auto own = [&](const int r) {
+            return r >= a && r < b && keep && !(exc && r >= xg.er0 && r < xg.er1);
+        };
+        // XG: the neighbouring waves of this role (the outer waves' outer
+        // edge lanes are halo: any value will do, their own slot)
+        const int rl = isA ? 0 : 1;
+        const int pw = pr, pme = pr + 1, pe = pr + 2;
+        // west neighbour of column c0 / east neighbour of column c0+1 of the
+        // row in ring slot i: DPP shifts, the edge lane's from the neighbouring
+        // wave's post (XG) or 0 (a halo lane)
+        auto nbw = [&](const double y, const int i) {
+            if (!XG || MGX_XG_DBG == 1) return dpp_shr1(y);
+            return dpp_shr1_or(y, xchy[rl][pw][i]);
+        };
+        auto nbe = [&](const double x, const int i) {
+            if (!XG || MGX_XG_DBG == 1) return dpp_shl1(x);
+            return dpp_shl1_or(x, xchx[rl][pe][i]);
+        };
+        // XG: at the end of a step at ring phase q, post lane 0's .x / lane
+        // 63's .y of the rows its stages changed (stage h, row slot q+1-h,
+        // updates .x iff its colour cs = 0) and of the row that entered the
+        // ring (slot q+3)
+        auto post_edges = [&](const double2 *ur, const int q) {
+            if (!XG || MGX_XG_DBG == 2) return;
+            if (l == 0) {
+#pragma unroll
+                for (int h = 0; h < S; ++h)
+                    if ((((q + 1 - h) & 1) ^ (h & 1)) == 0)
+                        xchx[rl][pme][(q + 1 - h + 2 * NR) % NR] = ur[(q + 1 - h + 2 * NR) % NR].x;
+                xchx[rl][pme][(q + 3) % NR] = ur[(q + 3) % NR].x;
+            }
+            if (l == 63) {
+#pragma unroll
+                for (int h = 0; h < S; ++h)
+                    if ((((q + 1 - h) & 1) ^ (h & 1)) == 1)
+                        xchy[rl][pme][(q + 1 - h + 2 * NR) % NR] = ur[(q + 1 - h + 2 * NR) % NR].y;
+                xchy[rl][pme][(q + 3) % NR] = ur[(q + 3) % NR].y;
+            }
+        };
         const bool in0 = act && c0 >= 1 && c0 <= n - 1;
         const bool in1 = act && c0 + 1 <= n - 1;
         const int cl = min(max(c0, 0), (int)pitch - 2);
@@ -1271,12 +1364,12 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             if (!GS) asm volatile("" : "+s"(cg.nu));
             // (the unguarded kernel only runs with d > 0: xsmooth_inst)
             if (cs == 0) {
-                const double uW = dpp_shr1(ur[iR].y);
+                const double uW = nbw(ur[iR].y, iR);
                 if (!GS || (inr && in0))
                     ur[iR].x = gs_point_t<!GS>(d.r.x, d.x.x, d.y.x, ur[iN].x, uW, ur[iS].x,
                                                ur[iR].y, cg);
             } else {
-                const double uE = dpp_shl1(ur[iR].x);
+                const double uE = nbe(ur[iR].x, iR);
                 if (!GS || (inr && in1))
                     ur[iR].y = gs_point_t<!GS>(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x,
                                                ur[iS].y, uE, cg);
@@ -1326,13 +1419,13 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             const double2 f = rd[iR].r;
             const bool inr = !GS || (r >= 1 && r <= n - 1);
             if (cs == 0) {
-                const double uW = dpp_shr1(ur[iR].y);
+                const double uW = nbw(ur[iR].y, iR);
                 if (!GS || (inr && in0))
                     ur[iR].x = div_diag<!GS>(f.x - k.cn.x * ur[iN].x - k.cw.x * uW -
                                                  k.cs.x * ur[iS].x - k.ce.x * ur[iR].y,
                                              c);
             } else {
-                const double uE = dpp_shl1(ur[iR].x);
+                const double uE = nbe(ur[iR].x, iR);
                 if (!GS || (inr && in1))
                     ur[iR].y = div_diag<!GS>(f.y - k.cn.y * ur[iN].y - k.cw.y * ur[iR].x -
                                                  k.cs.y * ur[iS].y - k.ce.y * uE,
@@ -1387,7 +1480,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         const int ro = s + 2 - S;
                         const double2 uf = ur[(p + 2 - S + 2 * NR) % NR];
                         uring[pr][(p + 2 - S + 2 * NR) % NU][l] = uf;
-                        st2_if(upost + (long)ro * pitch, c0, post && ro >= a && ro < b && keep,
+                        st2_if(upost + (long)ro * pitch, c0, post && own(ro),
                                uf);
                     }
                     // residual norm of u_post (multigrid.cpp:112-113), column c0 of
@@ -1399,8 +1492,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         const int iN = (p - S + 2 * NR) % NR;
                         const int iS = (p + 2 - S + 2 * NR) % NR;
                         const RowData &d = rd[iR];
-                        const double uW = dpp_shr1(ur[iR].y);
-                        const bool rin = r >= a && r < b;
+                        const double uW = nbw(ur[iR].y, iR);
                         // (with the row's coefficients: the same expressions, bitwise)
                         auto res0 = [&]() {
                             if (XACOEF) return res_x(iR, iN, iS, uW);
@@ -1408,18 +1500,19 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                                                ur[iS].x, ur[iR].y, c);
                         };
                         if (GN) {
-                            if (rin && keep && r >= 1 && r <= n - 1 && in0) {
+                            if (own(r) && r >= 1 && r <= n - 1 && in0) {
                                 const double res = res0();
                                 acc += res * res;
                             }
                         } else {   // acc + 0.0 == acc (acc >= +0): a select, no branch
                             const double r0 = res0();
-                            acc += (keep && rin) ? r0 * r0 : 0.0;
+                            acc += own(r) ? r0 * r0 : 0.0;
                         }
                     }
                     load_rv(s + XRV, (p + XRV) % NR);
+                    post_edges(ur, p);
+                    if (XG || (p & 1)) __syncthreads();
                     if (p & 1) {   // end of a pair (compile-time)
-                        __syncthreads();
                         it += 2;
                         if (it >= iters) goto done_a;
                     }
@@ -1448,10 +1541,9 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         const int r = s + 2;
                         const int iR = (q + 2) % NR, iN = (q + 1) % NR, iS = (q + 3) % NR;
                         const RowData &d = rd[iR];
-                        const double uE = dpp_shl1(ur[iR].x);
-                        const bool rin = r >= a && r < b;
+                        const double uE = nbe(ur[iR].x, iR);
                         if (GN) {
-                            if (rin && keep && r >= 1 && r <= n - 1 && in1) {
+                            if (own(r) && r >= 1 && r <= n - 1 && in1) {
                                 const double res =
                                     res_point_t(d.r.y, d.x.y, d.y.y, ur[iR].y, ur[iN].y,
                                                 ur[iR].x, ur[iS].y, uE, c);
@@ -1460,7 +1552,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         } else {   // acc + 0.0 == acc (acc >= +0): a select, no branch
                             const double r1 = res_point_t(d.r.y, d.x.y, d.y.y, ur[iR].y,
                                                           ur[iN].y, ur[iR].x, ur[iS].y, uE, c);
-                            acc += (keep && rin) ? r1 * r1 : 0.0;
+                            acc += own(r) ? r1 * r1 : 0.0;
                         }
                     }
                     if (RS) {
@@ -1472,7 +1564,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         const int r = s + 2;
                         const int iR = (q + 2) % NR, iN = (q + 1) % NR, iS = (q + 3) % NR;
                         RowData &d = rd[iR];
-                        const double uW = dpp_shr1(ur[iR].y), uE = dpp_shl1(ur[iR].x);
+                        const double uW = nbw(ur[iR].y, iR), uE = nbe(ur[iR].x, iR);
                         Coef cg = c;   // fresh nu: no coefficient CSE into the stages
                         asm volatile("" : "+s"(cg.nu));
                         const double f0 = rhs_point_t(d.x.x, d.y.x, ur[iR].x, ur[iN].x, uW,
@@ -1480,11 +1572,10 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         const double f1 = rhs_point_t(d.x.y, d.y.y, ur[iR].y, ur[iN].y, ur[iR].x,
                                                       ur[iS].y, uE, cg);
                         d.r = make_double2(f0, f1);
-                        const bool rin = r >= a && r < b;
                         const bool i0 = !GN || (r >= 1 && r <= n - 1 && in0);
                         const bool i1 = !GN || (r >= 1 && r <= n - 1 && in1);
                         double *row = rhs_next + (long)r * pitch;
-                        if (rin && keep) {
+                        if (own(r)) {
                             if (i0 && i1) {
                                 st2s(row + c0, d.r);
                             } else {
@@ -1496,15 +1587,15 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                                                       ur[iS].x, ur[iR].y, cg);
                         const double e1 = res_point_t(f1, d.x.y, d.y.y, ur[iR].y, ur[iN].y,
                                                       ur[iR].x, ur[iS].y, uE, cg);
-                        acc2 += (rin && keep && i0) ? e0 * e0 : 0.0;
-                        acc2 += (rin && keep && i1) ? e1 * e1 : 0.0;
+                        acc2 += (own(r) && i0) ? e0 * e0 : 0.0;
+                        acc2 += (own(r) && i1) ? e1 * e1 : 0.0;
                     }
                     to_coef(rd[(q + 1) % NR], cf[(q + 1) % NR]);   // row s+1
 #pragma unroll
                     for (int h = 0; h < S; ++h) stage_c(q, h, s + 1 - h);
                     {
                         const int ro = s + 2 - S;
-                        st2_if(upre + (long)ro * pitch, c0, ro >= a && ro < b && keep,
+                        st2_if(upre + (long)ro * pitch, c0, own(ro),
                                ur[(q + 2 - S + 2 * NR) % NR]);
                     }
                     if (((q + 1 - S) & 1) == 0) {   // compile-time row parity
@@ -1513,14 +1604,15 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         const int iR = (q + 1 - S + 2 * NR) % NR;
                         const int iN = (q - S + 2 * NR) % NR;
                         const int iS = (q + 2 - S + 2 * NR) % NR;
-                        const double uW = dpp_shr1(ur[iR].y);
-                        const bool on = r >= a && r < b && keep &&
+                        const double uW = nbw(ur[iR].y, iR);
+                        const bool on = own(r) &&
                                         (!GN || (r >= 1 && r <= n - 2 && in0 && c0 <= n - 2));
                         const double res = res_x(iR, iN, iS, uW);
                         st1_if(rhsc + (long)(r >> 1) * pitchc, c0 >> 1, on, res);
                     }
+                    post_edges(ur, q);
+                    if (XG || (p & 1)) __syncthreads();
                     if (p & 1) {
-                        __syncthreads();
                         it += 2;
                         if (it >= iters) goto done_b;
                     }
@@ -1536,7 +1628,19 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
         start += b - a;
         // a pair past its region's strips idles on the segment (A and B alike,
         // so each pair's barrier count still matches between its two waves)
-        if (__builtin_amdgcn_readfirstlane(strip) >= 0) march(strip * W, a, b);
+        if (__builtin_amdgcn_readfirstlane(strip) >= 0) {
+            if (XG) {
+                // group g = strips g*WPB .. g*WPB+WPB-1 (regions start at a
+                // multiple of WPB, so strip % WPB == pr); the last group is
+                // shifted left to end at xend and owns only what is left
+                const int g = strip / WPB;
+                const int k0 = xg.x0 + g * WGc;
+                const int og = g < xg.glast ? k0 : xg.xl;
+                march(og - 2 * H + 128 * pr, k0, g < xg.glast ? k0 + WGc : xg.xend, a, b);
+            } else {
+                march(strip * W - 2 * H, strip * W, strip * W + W, a, b);
+            }
+        }
     }
     const double tot = wave_sum(acc);   // one partial per wave (A: columns c0, B: c0+1)
     if (l == 0) partials[(long)blockIdx.x * 2 * WPB + wv] = tot;
@@ -2503,14 +2607,15 @@ static int smooth_winst(const SmoothArgs &A, hipStream_t s) {
 }
 
 
-template <int WPB, int K, bool G, bool RS = false, bool SV = false>
+template <int WPB, int K, bool G, bool RS = false, bool SV = false, bool XG = false>
 static int xsmooth_slots() {
     static int slots = 0;   // resident workgroups of this instantiation
     if (!slots) {
         int dev = 0, cus = 0, per = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_xsmooth<WPB, K, G, RS, SV>,
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per,
+                                                           k_xsmooth<WPB, K, G, RS, SV, XG>,
                                                            128 * WPB, 0);
         slots = std::max(1, cus) * std::max(1, per);
     }
@@ -2519,33 +2624,71 @@ static int xsmooth_slots() {
 
 // One launch over `reg`; min_rows: the fewest rows per workgroup (each
 // workgroup's march pays a warm-up of ~EA + EB + D rows).  Returns the norm
-// partials written (grid * 2 * WPB: one per wave) at `partials`.
-template <int WPB, int K, bool G, bool RS, bool SV>
+// partials written (grid * 2 * WPB: one per wave) at `partials`.  geo: the
+// group geometry (XG) or the guarded kernel's excluded rectangle.
+template <int WPB, int K, bool G, bool RS, bool SV, bool XG>
 static int xsmooth_launch_sv(const XArgs &A, const MarchRegions &reg, double *partials, int lo,
-                             int hi, long min_rows, long max_wgs, hipStream_t s) {
+                             int hi, long min_rows, long max_wgs, const XGeo &geo,
+                             hipStream_t s) {
     const long total = reg.pre[reg.count];
     if (total <= 0) return 0;
     long upw;
     MarchRegions r;
     using X = XCfg<K>;
-    const unsigned grid = plan_march(reg, WPB, xsmooth_slots<WPB, K, G, RS, SV>(), min_rows,
+    const unsigned grid = plan_march(reg, WPB, xsmooth_slots<WPB, K, G, RS, SV, XG>(), min_rows,
                                      max_wgs, X::EA + X::EB + X::D + X::NR / 2, upw, r);
     // RS: the second partials (the next step's initial norm) at the same
     // offsets, kNormBlocks further on
-    MGX_LAUNCH((k_xsmooth<WPB, K, G, RS, SV>), dim3(grid), dim3(128 * WPB), s, A.uin, A.upost,
-               A.upre, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch, r,
-               upw, A.c, lo, hi, A.store_post ? 1 : 0, A.rhs_next,
-               RS ? partials + kNormBlocks : (double *)nullptr, A.sa1, A.sb1, A.sa2, A.sb2);
+    MGX_LAUNCH((k_xsmooth<WPB, K, G, RS, SV, XG>), dim3(grid), dim3(128 * WPB), s, A.uin,
+               A.upost, A.upre, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n,
+               A.pitch, r, upw, A.c, lo, hi, A.store_post ? 1 : 0, A.rhs_next,
+               RS ? partials + kNormBlocks : (double *)nullptr, A.sa1, A.sb1, A.sa2, A.sb2, geo);
     return (int)grid * 2 * WPB;
 }
 // SV when the level's velocity factors are given (XArgs::sa1)
-template <int WPB, int K, bool G, bool RS = false>
+template <int WPB, int K, bool G, bool RS = false, bool XG = false>
 static int xsmooth_launch(const XArgs &A, const MarchRegions &reg, double *partials, int lo, int hi,
-                          long min_rows, long max_wgs, hipStream_t s) {
+                          long min_rows, long max_wgs, hipStream_t s,
+                          const XGeo &geo = XGeo{0, 0, 0, 0, 0, 0, 0, 0}) {
     if (A.sa1 && A.sb1 && A.sa2 && A.sb2)
-        return xsmooth_launch_sv<WPB, K, G, RS, true>(A, reg, partials, lo, hi, min_rows, max_wgs,
-                                                      s);
-    return xsmooth_launch_sv<WPB, K, G, RS, false>(A, reg, partials, lo, hi, min_rows, max_wgs, s);
+        return xsmooth_launch_sv<WPB, K, G, RS, true, XG>(A, reg, partials, lo, hi, min_rows,
+                                                          max_wgs, geo, s);
+    return xsmooth_launch_sv<WPB, K, G, RS, false, XG>(A, reg, partials, lo, hi, min_rows,
+                                                       max_wgs, geo, s);
+}
+
+long g_xgroup = 1;   // tuning key "xgroup": the group-exchange interior kernel (XG)
+void set_xgroup(long v) { g_xgroup = v; }
+long get_xgroup() { return g_xgroup; }
+
+// The XG launch's work: groups of WPB strips, each owning WGc = 128 WPB - 4H
+// columns, group 0 from column x0 = 2H + 2 (lane 0 on column 2, even), the
+// last group shifted left so that its last lane is column n-1 (owning what
+// the others leave up to xend), x rows [ma, mb); and the guarded kernel's
+// work around it in W-column strips: the strips holding columns [0, x0) and
+// [xend, n] on all rows, the others on the rows outside [ma, mb), with the
+// XG launch's rectangle excluded (XGeo::ec0..er1).  false: no group fits.
+template <int WPB, int K>
+static bool xg_regions(long n, int ra, int rb, int ma, int mb, MarchRegions &inner,
+                       MarchRegions &edge, XGeo &geo) {
+    using X = XCfg<K>;
+    constexpr int H = X::H, W = X::W, WGc = 128 * WPB - 4 * H;
+    inner = MarchRegions{};
+    edge = MarchRegions{};
+    const int x0 = 2 * H + 2;
+    const long xl = (n + 2 * H - 128 * WPB) & ~1L;
+    if (xl < x0 || mb <= ma) return false;
+    const int xend = (int)xl + WGc;
+    const int groups = (xend - x0 + WGc - 1) / WGc;
+    geo = XGeo{x0, (int)xl, xend, groups - 1, x0, xend, ma, mb};
+    add_region<WPB>(inner, 0, groups * WPB, ma, mb);
+    const int strips = (int)((n + 1 + W - 1) / W);
+    const int sl = (x0 + W - 1) / W, sr = std::min(strips, xend / W);
+    add_region<1>(edge, 0, sl, ra, rb);
+    add_region<1>(edge, sr, strips, ra, rb);
+    add_region<1>(edge, sl, sr, ra, ma);
+    add_region<1>(edge, sl, sr, mb, rb);
+    return true;
 }
 
 static void add_tile_region(TileRegions &r, int c0, int c1, int r0, int r1, int TR) {
@@ -2589,9 +2732,13 @@ static int xsmooth_tiled(const XArgs &A, int ra, int rb, int lo, int hi, hipStre
     xmargins<K>(A, ra, rb, top, bot);
     march_split(n, X::W, X::H, ra, rb, top, bot, si0, si1, ma, mb);
     TileRegions t{};
-    const bool inner_march = si1 > si0 && mb - ma >= kXTileAllRows;
+    MarchRegions ginner, gedge;
+    XGeo geo{};
+    const bool xg = g_xgroup != 0 && xg_regions<WPB, K>(n, ra, rb, ma, mb, ginner, gedge, geo);
+    const bool inner_march = (xg || si1 > si0) && mb - ma >= kXTileAllRows;
     if (inner_march) {
-        const int ca = si0 * X::W, cb = (int)std::min<long>(n + 1, (long)si1 * X::W);
+        const int ca = xg ? geo.x0 : si0 * X::W;
+        const int cb = xg ? geo.xend : (int)std::min<long>(n + 1, (long)si1 * X::W);
         add_tile_region(t, 0, ca, ra, rb, kXTileRows);
         add_tile_region(t, cb, (int)n + 1, ra, rb, kXTileRows);
         add_tile_region(t, ca, cb, ra, ma, kXTileRows);
@@ -2604,10 +2751,16 @@ static int xsmooth_tiled(const XArgs &A, int ra, int rb, int lo, int hi, hipStre
     if (tiles > kNormBlocks / 2) return -2;   // too many: the caller marches the edges
     int pm = A.phase == 2 ? A.partials_done : 0;
     if (inner_march && A.phase != 2) {
-        MarchRegions inner{};
-        add_region<WPB>(inner, si0, si1, ma, mb);
-        pm = xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, A.min_rows,
-                                           kNormBlocks / (2 * WPB) / 2, s);
+        if (xg) {
+            pm = xsmooth_launch<WPB, K, false, false, true>(A, ginner, A.partials, lo, hi,
+                                                            A.min_rows,
+                                                            kNormBlocks / (2 * WPB) / 2, s, geo);
+        } else {
+            MarchRegions inner{};
+            add_region<WPB>(inner, si0, si1, ma, mb);
+            pm = xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, A.min_rows,
+                                               kNormBlocks / (2 * WPB) / 2, s);
+        }
     }
     if (A.phase == 1) return pm;
     if (tiles > 0)
@@ -2637,6 +2790,16 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
         if (g_xfast == 0 || !(A.c.dgs > 0) || A.rb >= 0 || rb - ra <= g_xtile_max_rows)
             return -3;
         MarchRegions inner, edge, unused;
+        XGeo geo{};
+        const int ma = std::max(ra, X::TOP_RS), mb = std::min(rb, (int)n + 1 - X::BOT);
+        if (g_xgroup != 0 && xg_regions<WPB, K>(n, ra, rb, ma, mb, inner, edge, geo)) {
+            const int pm = xsmooth_launch<WPB, K, false, true, true>(
+                A, inner, A.partials, lo, hi, A.min_rows, kNormBlocks / (2 * WPB) / 2, s, geo);
+            const int pe = xsmooth_launch<1, K, true, true>(A, edge, A.partials + pm, lo, hi,
+                                                            std::min(32, A.min_rows),
+                                                            kNormBlocks / 2 / 2, s, geo);
+            return pm + pe;
+        }
         march_regions<WPB>(n, X::W, X::H, ra, rb, X::TOP_RS, X::BOT, true, inner, unused);
         march_regions<1>(n, X::W, X::H, ra, rb, X::TOP_RS, X::BOT, true, unused, edge);
         const int pm = xsmooth_launch<WPB, K, false, true>(A, inner, A.partials, lo, hi,
@@ -2661,16 +2824,25 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
     }
     int top, bot;
     xmargins<K>(A, ra, rb, top, bot);
-    march_regions<WPB>(n, X::W, X::H, ra, rb, top, bot, split, inner, unused);
-    march_regions<1>(n, X::W, X::H, ra, rb, top, bot, split, unused, edge);
-    const int pm = A.phase == 2 ? A.partials_done
-                                : xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi,
-                                                                A.min_rows,
-                                                                kNormBlocks / (2 * WPB) / 2, s);
+    XGeo geo{};
+    const int ma = std::max(ra, top), mb = std::min(rb, (int)n + 1 - bot);
+    const bool xg =
+        split && g_xgroup != 0 && xg_regions<WPB, K>(n, ra, rb, ma, mb, inner, edge, geo);
+    if (!xg) {
+        march_regions<WPB>(n, X::W, X::H, ra, rb, top, bot, split, inner, unused);
+        march_regions<1>(n, X::W, X::H, ra, rb, top, bot, split, unused, edge);
+    }
+    int pm = A.partials_done;
+    if (A.phase != 2)
+        pm = xg ? xsmooth_launch<WPB, K, false, false, true>(A, inner, A.partials, lo, hi,
+                                                             A.min_rows,
+                                                             kNormBlocks / (2 * WPB) / 2, s, geo)
+                : xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, A.min_rows,
+                                                kNormBlocks / (2 * WPB) / 2, s);
     if (A.phase == 1) return pm;
     const int pe = xsmooth_launch<1, K, true>(A, edge, A.partials + pm, lo, hi,
                                               std::min(MGX_XEDGE_ROWS, A.min_rows),
-                                              kNormBlocks / 2 / 2, s);
+                                              kNormBlocks / 2 / 2, s, geo);
     return pm + pe;
 }
 

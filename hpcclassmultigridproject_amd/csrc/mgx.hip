@@ -1363,6 +1363,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgx::set_xfast(value);
         return MGX_OK;
     }
+    if (!strcmp(key, "xgroup")) {
+        if (value != 0 && value != 1) return fail(MGX_E_ARG, "xgroup must be 0 or 1");
+        mgx::set_xgroup(value);
+        return MGX_OK;
+    }
     if (!strcmp(key, "tile32_min_n")) {
         if (value < 0) return fail(MGX_E_ARG, "tile32_min_n must be >= 0");
         mgx::set_tile32_min_n(value);
@@ -1456,6 +1461,10 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "xfast")) {
         *value = mgx::get_xfast();
+        return MGX_OK;
+    }
+    if (!strcmp(key, "xgroup")) {
+        *value = mgx::get_xgroup();
         return MGX_OK;
     }
     if (!strcmp(key, "tile32_min_n")) {

@@ -48,9 +48,14 @@ for r in range(a.rounds):
         for k, v in old.items():
             _lib.set_tuning(k, v)
 for st, kv, mg in ctx:
+    old = {k: _lib.get_tuning(k) for k in kv}
+    for k, v in kv.items():   # launch-time keys apply to the profiled cycles too
+        _lib.set_tuning(k, int(v))
     mg.profile_reset()
     mg.profile(True)
     mg.run_cycles(3)
+    for k, v in old.items():
+        _lib.set_tuning(k, v)
     lv = []
     for l in range(L):
         tot = 0.0
