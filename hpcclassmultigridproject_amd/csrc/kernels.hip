@@ -1162,6 +1162,11 @@ struct XCfg {
 // edge lane takes the posted value through the DPP shift's "keep old" form
 // (bound_ctrl off): no extra VALU instruction.  The halo work of the pass
 // drops from 28 of 128 columns to 28 of 512.
+// rhs row prefetch distance of the XG kernel (its exchange values take the
+// registers of one prefetched row)
+#ifndef MGX_XGRV
+#define MGX_XGRV 3
+#endif
 #ifndef MGX_XG_DBG
 #define MGX_XG_DBG 0
 #endif
@@ -1190,7 +1195,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     // pass is bound by loads in flight, not by VALU: rhs/v 2 -> 3 -> 4 steps
     // took level 0 -4 % and -3 % at the same VGPR count (B's path sets it);
     // u 3-4 steps or rhs/v 5 measured no better (N=16384, tools/ab_libs.sh).
-    constexpr int XRV = MGX_XRV;
+    constexpr int XRV = XG ? MGX_XGRV : MGX_XRV;
     constexpr int XU = MGX_XU;
     // A forms each row's coefficients once (MGX_XACOEF; B always does).  Not
     // in the guarded edge kernel: there it takes the kernel past 256 VGPRs
@@ -1208,8 +1213,8 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     // (entries 0 and WPB+1 of each role: the outer waves' outer neighbours,
     // never written -- read only by halo lanes -- so that a wave's own, west
     // and east entries sit at fixed offsets from one address)
-    __shared__ double xchx[XG ? 2 : 1][XG ? WPB + 2 : 1][XG ? NR : 1],
-        xchy[XG ? 2 : 1][XG ? WPB + 2 : 1][XG ? NR : 1];
+    // [role][wave + 1][0: lane 0's .x, 1: lane 63's .y][slot]
+    __shared__ double xch[XG ? 2 : 1][XG ? WPB + 2 : 1][2][XG ? NR : 1];
 
     const int l = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
@@ -1244,11 +1249,11 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
         // wave's post (XG) or 0 (a halo lane)
         auto nbw = [&](const double y, const int i) {
             if (!XG || MGX_XG_DBG == 1) return dpp_shr1(y);
-            return dpp_shr1_or(y, xchy[rl][pw][i]);
+            return dpp_shr1_or(y, xch[rl][pw][1][i]);
         };
         auto nbe = [&](const double x, const int i) {
             if (!XG || MGX_XG_DBG == 1) return dpp_shl1(x);
-            return dpp_shl1_or(x, xchx[rl][pe][i]);
+            return dpp_shl1_or(x, xch[rl][pe][0][i]);
         };
         // XG: at the end of a step at ring phase q, post lane 0's .x / lane
         // 63's .y of the rows its stages changed (stage h, row slot q+1-h,
@@ -1260,15 +1265,15 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
 #pragma unroll
                 for (int h = 0; h < S; ++h)
                     if ((((q + 1 - h) & 1) ^ (h & 1)) == 0)
-                        xchx[rl][pme][(q + 1 - h + 2 * NR) % NR] = ur[(q + 1 - h + 2 * NR) % NR].x;
-                xchx[rl][pme][(q + 3) % NR] = ur[(q + 3) % NR].x;
+                        xch[rl][pme][0][(q + 1 - h + 2 * NR) % NR] = ur[(q + 1 - h + 2 * NR) % NR].x;
+                xch[rl][pme][0][(q + 3) % NR] = ur[(q + 3) % NR].x;
             }
             if (l == 63) {
 #pragma unroll
                 for (int h = 0; h < S; ++h)
                     if ((((q + 1 - h) & 1) ^ (h & 1)) == 1)
-                        xchy[rl][pme][(q + 1 - h + 2 * NR) % NR] = ur[(q + 1 - h + 2 * NR) % NR].y;
-                xchy[rl][pme][(q + 3) % NR] = ur[(q + 3) % NR].y;
+                        xch[rl][pme][1][(q + 1 - h + 2 * NR) % NR] = ur[(q + 1 - h + 2 * NR) % NR].y;
+                xch[rl][pme][1][(q + 3) % NR] = ur[(q + 3) % NR].y;
             }
         };
         const bool in0 = act && c0 >= 1 && c0 <= n - 1;
