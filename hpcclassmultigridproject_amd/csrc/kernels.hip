@@ -118,6 +118,33 @@ __device__ __forceinline__ void st2_if(double *row, int col, bool on, double2 v)
 __device__ __forceinline__ void st1_if(double *row, int col, bool on, double v) {
     if (on) row[col] = v;
 }
+// The same accesses as a uniform row base + a per-lane unsigned byte offset:
+// the saddr form of global_load / global_store (SGPR base, 32-bit VGPR
+// offset) instead of a 64-bit per-lane address -- no 64-bit address add per
+// access, and the march keeps one offset register per column instead of a
+// pointer pair per field.  (Lanes whose offset would be negative are never
+// enabled: `on` implies an owned column.)
+__device__ __forceinline__ const char *rowb(const double *row, unsigned boff) {
+    return reinterpret_cast<const char *>(row) + boff;
+}
+__device__ __forceinline__ double2 ld2u(const double *row, unsigned boff) {
+    return *reinterpret_cast<const double2 *>(rowb(row, boff));
+}
+__device__ __forceinline__ double ld1u(const double *row, unsigned boff) {
+    return *reinterpret_cast<const double *>(rowb(row, boff));
+}
+__device__ __forceinline__ void st2_ifu(double *row, int col, bool on, double2 v) {
+    double *p = reinterpret_cast<double *>(const_cast<char *>(rowb(row, (unsigned)col * 8u)));
+#if MGX_NTST
+    if (on) st2s(p, v);
+#else
+    if (on) st2(p, v);
+#endif
+}
+__device__ __forceinline__ void st1_ifu(double *row, int col, bool on, double v) {
+    double *p = reinterpret_cast<double *>(const_cast<char *>(rowb(row, (unsigned)col * 8u)));
+    if (on) *p = v;
+}
 __device__ __forceinline__ double sel(double2 p, int s) {
     const double x = p.x, y = p.y;
     return s ? y : x;
@@ -1281,6 +1308,9 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
         const int cl = min(max(c0, 0), (int)pitch - 2);
         const int jl = cl >> 1;
         const int j1 = (jl + 1 <= nc) ? 1 : 0;
+        // per-lane byte offsets of the loads (uniform row bases: saddr form)
+        const unsigned bcl = (unsigned)cl * 8u, bjl = (unsigned)jl * 8u,
+                       bjl1 = (unsigned)(jl + j1) * 8u;
 
         struct UPre {
             double2 X;
@@ -1295,13 +1325,13 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
         // an even row needs only the coarse row below it)
         auto load_u = [&](int R, UPre &u, const bool odd) {
             const int Rc = min(max(R, lo), hi);
-            u.X = ld2((uin + (long)Rc * pitch) + cl);
-            const double *p0 = (uc + (long)(Rc >> 1) * pitchc) + jl;
-            u.q00 = p0[0];
-            u.q01 = p0[j1];
+            u.X = ld2u(uin + (long)Rc * pitch, bcl);
+            const double *p0 = uc + (long)(Rc >> 1) * pitchc;
+            u.q00 = ld1u(p0, bjl);
+            u.q01 = ld1u(p0, bjl1);
             if (odd) {
-                u.q10 = p0[pitchc];
-                u.q11 = p0[pitchc + j1];
+                u.q10 = ld1u(p0 + pitchc, bjl);
+                u.q11 = ld1u(p0 + pitchc, bjl1);
             }
         };
         // + prolongation (gs.cpp:238-265); static parity, select (see k_wsmooth)
@@ -1337,7 +1367,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             const int Rc = min(max(R, lo), hi);
             const long o = (long)Rc * pitch;
             RowData &d = rd[q];
-            d.r = ld2((rhs + o) + cl);
+            d.r = ld2u(rhs + o, bcl);
             if (SV) {
                 ar1[q] = sa1[Rc];
                 ar2[q] = sa2[Rc];
@@ -1384,7 +1414,10 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
         // A's first step (aligned to NR so ring indices and parities are
         // static); B runs D steps behind; the last iteration is B's last step
         // (rounded up to whole pairs: an extra step stores nothing)
-        int s0 = a - EB - EA - (RS ? 1 : 0);
+        // (XG: 2 rows earlier -- the prologue's first rows s0+1, s0+2 enter
+        // the ring unposted, so the neighbouring waves' warm-up garbage
+        // reaches 2 rows further down than a lone strip's)
+        int s0 = a - EB - EA - (RS ? 1 : 0) - (XG ? 2 : 0);
         s0 = s0 >= 0 ? (s0 / NR) * NR : -(((-s0) + NR - 1) / NR) * NR;
         s0 = __builtin_amdgcn_readfirstlane(s0);
         const int iters = ((b + EB - 3) + D - s0 + 1 + 1) & ~1;
@@ -1485,7 +1518,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         const int ro = s + 2 - S;
                         const double2 uf = ur[(p + 2 - S + 2 * NR) % NR];
                         uring[pr][(p + 2 - S + 2 * NR) % NU][l] = uf;
-                        st2_if(upost + (long)ro * pitch, c0, post && own(ro),
+                        st2_ifu(upost + (long)ro * pitch, c0, post && own(ro),
                                uf);
                     }
                     // residual norm of u_post (multigrid.cpp:112-113), column c0 of
@@ -1499,7 +1532,18 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         const RowData &d = rd[iR];
                         const double uW = nbw(ur[iR].y, iR);
                         // (with the row's coefficients: the same expressions, bitwise)
+                        // XG: the row's rhs / t1 / t2 from the hand-off ring
+                        // (B takes them two steps later) and the coefficients
+                        // formed here -- 8 fp64 ops more, but A keeps neither
+                        // the row's coefficients nor its rhs for this step: 20
+                        // VGPRs fewer on A's path, which sets the kernel's count
                         auto res0 = [&]() {
+                            if (XG) {
+                                double2(*slot)[64] = rdring[pr][(p + 1 - S + 2 * NRD) % NRD];
+                                const double2 fr = slot[0][l], f1 = slot[1][l], f2 = slot[2][l];
+                                return res_point_t(fr.x, f1.x, f2.x, ur[iR].x, ur[iN].x, uW,
+                                                   ur[iS].x, ur[iR].y, c);
+                            }
                             if (XACOEF) return res_x(iR, iN, iS, uW);
                             return res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x, ur[iN].x, uW,
                                                ur[iS].x, ur[iR].y, c);
@@ -1600,7 +1644,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                     for (int h = 0; h < S; ++h) stage_c(q, h, s + 1 - h);
                     {
                         const int ro = s + 2 - S;
-                        st2_if(upre + (long)ro * pitch, c0, own(ro),
+                        st2_ifu(upre + (long)ro * pitch, c0, own(ro),
                                ur[(q + 2 - S + 2 * NR) % NR]);
                     }
                     if (((q + 1 - S) & 1) == 0) {   // compile-time row parity
@@ -1613,7 +1657,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         const bool on = own(r) &&
                                         (!GN || (r >= 1 && r <= n - 2 && in0 && c0 <= n - 2));
                         const double res = res_x(iR, iN, iS, uW);
-                        st1_if(rhsc + (long)(r >> 1) * pitchc, c0 >> 1, on, res);
+                        st1_ifu(rhsc + (long)(r >> 1) * pitchc, c0 >> 1, on, res);
                     }
                     post_edges(ur, q);
                     if (XG || (p & 1)) __syncthreads();
@@ -2674,9 +2718,11 @@ long get_xgroup() { return g_xgroup; }
 // [xend, n] on all rows, the others on the rows outside [ma, mb), with the
 // XG launch's rectangle excluded (XGeo::ec0..er1).  false: no group fits.
 template <int WPB, int K>
-static bool xg_regions(long n, int ra, int rb, int ma, int mb, MarchRegions &inner,
+static bool xg_regions(long n, int ra, int rb, int top, int bot, MarchRegions &inner,
                        MarchRegions &edge, XGeo &geo) {
     using X = XCfg<K>;
+    // the XG march starts 2 rows earlier (k_xsmooth): 2 more margin rows
+    const int ma = std::max(ra, top + 2), mb = std::min(rb, (int)n + 1 - bot);
     constexpr int H = X::H, W = X::W, WGc = 128 * WPB - 4 * H;
     inner = MarchRegions{};
     edge = MarchRegions{};
@@ -2739,7 +2785,8 @@ static int xsmooth_tiled(const XArgs &A, int ra, int rb, int lo, int hi, hipStre
     TileRegions t{};
     MarchRegions ginner, gedge;
     XGeo geo{};
-    const bool xg = g_xgroup != 0 && xg_regions<WPB, K>(n, ra, rb, ma, mb, ginner, gedge, geo);
+    const bool xg = g_xgroup != 0 && xg_regions<WPB, K>(n, ra, rb, top, bot, ginner, gedge, geo);
+    if (xg) ma = geo.er0;   // the XG march's rows: [er0, er1)
     const bool inner_march = (xg || si1 > si0) && mb - ma >= kXTileAllRows;
     if (inner_march) {
         const int ca = xg ? geo.x0 : si0 * X::W;
@@ -2795,16 +2842,8 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
         if (g_xfast == 0 || !(A.c.dgs > 0) || A.rb >= 0 || rb - ra <= g_xtile_max_rows)
             return -3;
         MarchRegions inner, edge, unused;
-        XGeo geo{};
-        const int ma = std::max(ra, X::TOP_RS), mb = std::min(rb, (int)n + 1 - X::BOT);
-        if (g_xgroup != 0 && xg_regions<WPB, K>(n, ra, rb, ma, mb, inner, edge, geo)) {
-            const int pm = xsmooth_launch<WPB, K, false, true, true>(
-                A, inner, A.partials, lo, hi, A.min_rows, kNormBlocks / (2 * WPB) / 2, s, geo);
-            const int pe = xsmooth_launch<1, K, true, true>(A, edge, A.partials + pm, lo, hi,
-                                                            std::min(32, A.min_rows),
-                                                            kNormBlocks / 2 / 2, s, geo);
-            return pm + pe;
-        }
+        // (the time-step mode keeps the separate strips: its B wave's extra
+        // stage takes the XG kernel past 256 VGPRs)
         march_regions<WPB>(n, X::W, X::H, ra, rb, X::TOP_RS, X::BOT, true, inner, unused);
         march_regions<1>(n, X::W, X::H, ra, rb, X::TOP_RS, X::BOT, true, unused, edge);
         const int pm = xsmooth_launch<WPB, K, false, true>(A, inner, A.partials, lo, hi,
@@ -2830,9 +2869,8 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
     int top, bot;
     xmargins<K>(A, ra, rb, top, bot);
     XGeo geo{};
-    const int ma = std::max(ra, top), mb = std::min(rb, (int)n + 1 - bot);
     const bool xg =
-        split && g_xgroup != 0 && xg_regions<WPB, K>(n, ra, rb, ma, mb, inner, edge, geo);
+        split && g_xgroup != 0 && xg_regions<WPB, K>(n, ra, rb, top, bot, inner, edge, geo);
     if (!xg) {
         march_regions<WPB>(n, X::W, X::H, ra, rb, top, bot, split, inner, unused);
         march_regions<1>(n, X::W, X::H, ra, rb, top, bot, split, unused, edge);
