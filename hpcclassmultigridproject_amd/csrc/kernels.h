@@ -140,8 +140,8 @@ bool xstep_supported(long n);
 void set_xfast(long v);
 long get_xfast();
 // Cross pass interior kernel: 1 = the group-exchange form (a workgroup's strips
-// adjacent, edge columns through LDS: 28 halo columns per 512), 0 = separate
-// strips with their own halos (28 per 128).  Bitwise the same.
+// adjacent, edge columns through LDS: 28 halo columns per 512), 0 (default) =
+// separate strips with their own halos (28 per 128).  Bitwise the same.
 void set_xgroup(long v);
 long get_xgroup();
 void set_march_tile_rows(long v);

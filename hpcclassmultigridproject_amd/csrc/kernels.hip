@@ -2706,7 +2706,12 @@ static int xsmooth_launch(const XArgs &A, const MarchRegions &reg, double *parti
                                                        max_wgs, geo, s);
 }
 
-long g_xgroup = 1;   // tuning key "xgroup": the group-exchange interior kernel (XG)
+// tuning key "xgroup": the group-exchange interior kernel (XG), default off:
+// bitwise, 13 % less VALU per owned point (28 halo columns per 512 instead of
+// per 128), but level 0 2.09 vs 1.88 ms at N=16384 -- the per-step barrier
+// and the exchange reads' LDS latency on every stage chain (at 250 VGPRs the
+// reads cannot be issued ahead) cost more than the halo work saved
+long g_xgroup = 0;
 void set_xgroup(long v) { g_xgroup = v; }
 long get_xgroup() { return g_xgroup; }
 

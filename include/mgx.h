@@ -179,10 +179,10 @@ int mgx_synchronize(mgx_ctx *ctx);
  * "xfast": 1 (default) runs the cross-cycle pass as an unguarded kernel over
  * the interior strips and rows plus a guarded kernel over the boundary strips
  * and bands; 0 = one guarded launch (bitwise the same results).
- * "xgroup": 1 (default) runs that interior kernel as groups of four adjacent
- * 128-column strips exchanging their edge columns through LDS (the halo of the
- * temporal blocking only on the group's outer sides); 0 = independent strips,
- * each with its own halo (bitwise the same results).
+ * "xgroup": 1 runs that interior kernel as groups of four adjacent 128-column
+ * strips exchanging their edge columns through LDS (the halo of the temporal
+ * blocking only on the group's outer sides); 0 (default) = independent strips,
+ * each with its own halo (bitwise the same results; 0 is faster on MI355X).
  * "march_tile_rows": a row block whose wave march would give each resident
  * workgroup fewer than this many rows runs as LDS tiles (default 16, >= 0).
  * "xtile_max_rows": on row blocks of at most this many rows (a rank of a

@@ -240,3 +240,29 @@ def test_one_segment_per_workgroup_plan(N, L, G, cross, knobs):
     u1_, n1 = _cycles_plain(N, L, 3, **kw)
     assert np.array_equal(u0_, u1_)
     np.testing.assert_allclose(n1, n0, rtol=NORM_RTOL)
+
+
+@pytest.mark.parametrize("N,L,cyc", [(8192, 3, 4), (4096, 6, 4)], ids=["split", "tiled"])
+def test_group_exchange_is_bitwise(N, L, cyc):
+    """Tuning key "xgroup": the interior cross pass as groups of four adjacent
+    strips exchanging their edge columns through LDS (k_xsmooth<..., XG>).
+    u, and the norms to 1e-11, equal the separate-strip kernel's after several
+    cycles -- N=8192, L=3 has march segments starting 14 rows below their
+    first aligned step (band starts 584, 3294, 6004), where the round-3 first
+    version leaked warm-up garbage into the restriction; N=4096 runs the XG
+    march beside k_xtile edge tiles."""
+    old = _lib.get_tuning("xgroup")
+    out = {}
+    try:
+        for xg in (0, 1):
+            _lib.set_tuning("xgroup", xg)
+            u0, v1, v2 = init_problem(N)
+            with Multigrid(N, L, 1.0 / N / 10, NU) as mg:
+                mg.upload(u0, v1, v2)
+                mg.rhs()
+                norms = [mg.run_cycles(1) for _ in range(cyc)]
+                out[xg] = (mg.download(), norms)
+    finally:
+        _lib.set_tuning("xgroup", old)
+    assert np.array_equal(out[0][0], out[1][0])
+    np.testing.assert_allclose(out[1][1], out[0][1], rtol=NORM_RTOL)
