@@ -54,8 +54,8 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s HBM3E
 # PMC traffic summary committed under profiles/ (tools/profile_round.sh)
 # (the cross pass is two launches: the unguarded interior kernel and the
 # guarded edge kernel; their traffic is summed)
-KERNEL_IDS = {(8, 0): ("mgx::k_xsmooth<4, 3, false, false, true>",
-                       "mgx::k_xsmooth<1, 3, true, false, true>"),
+KERNEL_IDS = {(8, 0): ("mgx::k_xsmooth<4, 3, false, false, true, false>",
+                       "mgx::k_xsmooth<1, 3, true, false, true, false>"),
               (0, 0): ("mgx::k_wsmooth<4, 3, 4, true>",),
               (7, 0): ("mgx::k_wsmooth<4, 3, 10, true>",)}
 KERNELS_HIP = os.path.join(ROOT, "hpcclassmultigridproject_amd", "csrc", "kernels.hip")
@@ -81,9 +81,10 @@ def traffic_profile():
                   "(regenerate with tools/profile_round.sh)")
 
 
-def lookup_traffic(knames):
-    """HBM bytes per dispatch of the finest-level instances (largest traffic) of
-    the kernels in knames, summed (one launch of the op = one dispatch of each)."""
+def lookup_traffic(knames, field="hbm_bytes"):
+    """HBM bytes (or another per-dispatch PMC field) of the finest-level
+    instances (largest traffic) of the kernels in knames, summed (one launch of
+    the op = one dispatch of each)."""
     path, kernels = traffic_profile()
     if path is None:
         return None, None, kernels
@@ -92,11 +93,11 @@ def lookup_traffic(knames):
         best = None
         for key, v in kernels.items():
             if key.split(" grid=")[0] == kname and (best is None or v["hbm_bytes"] > best[1]):
-                best = (key, v["hbm_bytes"])
-        if best is None:
-            return None, None, f"{kname} not in {path}"
+                best = (key, v["hbm_bytes"], v.get(field))
+        if best is None or best[2] is None:
+            return None, None, f"{kname} ({field}) not in {path}"
         keys.append(best[0])
-        total += best[1]
+        total += best[2]
     return " + ".join(keys), total, path
 
 
@@ -466,6 +467,18 @@ def main():
             roof["hbm_GBs"] = round(traffic / avg_s / 1e9, 1)
             roof["hbm_frac"] = round(traffic / avg_s / 1e9 / HBM_PEAK_GBS, 4)
             roof["traffic_over_compulsory"] = round(traffic / per_launch, 3)
+            # the pass is bound by its instruction stream more than by bytes:
+            # VALU instructions per launch (PMC SQ_INSTS_VALU, same profile)
+            # against the issue capacity in its live duration (one wave
+            # instruction per 4 cycles per SIMD, 1024 SIMDs, 2.4 GHz peak clock:
+            # a lower bound on the busy fraction)
+            _, valu, _ = lookup_traffic(ids, "SQ_INSTS_VALU")
+            if valu:
+                cap = 1024 * avg_s * 2.4e9 / 4
+                roof["valu"] = {"insts_per_launch": valu, "issue_capacity": round(cap),
+                                "issue_frac": round(valu / cap, 4),
+                                "note": "VALU wave-instructions / (1024 SIMDs x 2.4 GHz / 4 "
+                                        "cycles per wave64 op x live mean duration)"}
         else:
             roof["traffic_null_reason"] = tsrc
 
