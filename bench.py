@@ -494,6 +494,17 @@ def main():
         roof["achieved_frac_of_stream5"] = round(roof["achieved"] / roof["stream5_ceiling_GBs"], 4)
         if "hbm_GBs" in roof:
             roof["hbm_frac_of_stream5"] = round(roof["hbm_GBs"] / roof["stream5_ceiling_GBs"], 4)
+    if roof is not None and fac.value and world == 1:
+        # the same pass's bytes if v1, v2 were read as 2-D arrays (the
+        # reference algorithm's inputs, SURVEY 8(d): GS reads u, rhs, v1, v2):
+        # the velocity factors regenerate them bitwise instead of reading them
+        vb = 2.0 * 8.0 * (N + 1) * ((N + 1 + 15) // 16 * 16)
+        a2 = (roof["compulsory_bytes_per_launch"] + vb) / (roof["avg_launch_ms"] * 1e-3) / 1e9
+        roof["algorithmic_2d_velocity"] = {
+            "bytes_per_launch": roof["compulsory_bytes_per_launch"] + vb,
+            "GBs": round(a2, 1), "frac": round(a2 / HBM_PEAK_GBS, 4),
+            "note": "compulsory bytes with v1, v2 counted as read (they are regenerated "
+                    "bitwise from their rank-1 factors instead)"}
     out = {
         "metric": f"V-cycle grid-point-updates/sec at N={N}; achieved HBM GB/s vs peak",
         "value": value, "unit": "grid-point-updates/s", "n_gpus": world,
