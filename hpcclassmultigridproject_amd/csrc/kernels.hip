@@ -2894,10 +2894,6 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
     return pm + pe;
 }
 
-// strip pairs per workgroup of the interior cross pass (experiment builds)
-#ifndef MGX_XWPB
-#define MGX_XWPB 4
-#endif
 int launch_xsmooth(const XArgs &A, int sweeps, hipStream_t s) {
     if (A.rb >= 0 && (A.ra & 1)) return -1;   // row blocks start at even rows
     int blocks = -1;
@@ -2905,8 +2901,8 @@ int launch_xsmooth(const XArgs &A, int sweeps, hipStream_t s) {
     // 1-KiB row pieces of four strips per load (measured: 4.05 ms vs 4.13 ms
     // with 2 pairs, N=16384)
     switch (sweeps) {
-        case 2: blocks = xsmooth_inst<MGX_XWPB, 2>(A, s); break;
-        case 3: blocks = xsmooth_inst<MGX_XWPB, 3>(A, s); break;
+        case 2: blocks = xsmooth_inst<4, 2>(A, s); break;
+        case 3: blocks = xsmooth_inst<4, 3>(A, s); break;
         default: return -1;
     }
     if (A.phase == 1) return blocks;   // the norm comes with phase 2
