@@ -779,9 +779,15 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
     const int nc = n >> 1;
     const double hh = c.h * 0.5;
     double acc = 0.0;
+    // row offsets as 32 x 32 -> 64-bit products (pitches < 2^31 elements)
+    const int ip = (int)pitch, ipc = (int)pitchc;
+    auto rowoff = [](int r, int p) { return (long)r * (long)p; };
+    int a = 0, b = 0;   // the segment's owned rows (set per segment below)
+    // r in [a, b) as one unsigned compare (b >= a)
+    auto rowin = [&](int r) { return (unsigned)(r - a) < (unsigned)(b - a); };
 
     while (start < end) {
-        int strip, a, b;
+        int strip;   // a, b: the segment's rows (captured by rowin)
         region_segment(reg, WPB, wv, start, end, strip, a, b);
         start += b - a;
         if (__builtin_amdgcn_readfirstlane(strip) < 0) continue;
@@ -807,14 +813,14 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
         auto load_u = [&](int R, UPre &u, const bool odd) {
             if (C::ZERO) return;
             const int Rc = min(max(R, lo), hi);
-            u.X = ld2((uin + (long)Rc * pitch) + cl);
+            u.X = ld2((uin + rowoff(Rc, ip)) + cl);
             if (C::PROL) {
-                const double *p0 = (uc + (long)(Rc >> 1) * pitchc) + jl;
+                const double *p0 = (uc + rowoff(Rc >> 1, ipc)) + jl;
                 u.q00 = p0[0];
                 u.q01 = p0[j1];
                 if (odd) {
-                    u.q10 = p0[pitchc];
-                    u.q11 = p0[pitchc + j1];
+                    u.q10 = p0[ipc];
+                    u.q11 = p0[ipc + j1];
                 }
             }
         };
@@ -849,7 +855,7 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
         // zero row -- a uniform select, the load stays unconditional)
         auto load_rv = [&](int R, RowData &d) {
             const int Rc = min(max(R, lo), hi);
-            const long o = (long)Rc * pitch;
+            const long o = rowoff(Rc, ip);
             if (!C::RHSN) d.r = ld2((rhs + o) + cl);
             const bool z = Rc >= vz;
             d.x = ld2((z ? zrow : v1 + o) + cl);
@@ -927,8 +933,8 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
             const double f1 = rhs_point_t(d.x.y, d.y.y, ur[iR].y, ur[iN].y, ur[iR].x, ur[iS].y,
                                           uE, cg);
             d.r = make_double2(f0, f1);
-            if (r >= a && r < b && r >= 1 && r <= n - 1 && keep) {
-                double *row = rhs_out + (long)r * pitch;
+            if (rowin(r) && r >= 1 && r <= n - 1 && keep) {
+                double *row = rhs_out + rowoff(r, ip);
                 if (in0 && in1) {
                     st2(row + c0, d.r);
                 } else {
@@ -1025,7 +1031,7 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                 // (3) row s+2-S is final
                 {
                     const int ro = s + 2 - S;
-                    st2_if(uout + (long)ro * pitch, c0, ro >= a && ro < b && keep,
+                    st2_if(uout + rowoff(ro, ip), c0, rowin(ro) && keep,
                            ur[(p + 2 - S + 2 * NR) % NR]);
                 }
                 // (4) residual stage on row s+1-S
@@ -1043,10 +1049,10 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                                            ur[iR].y, c);
                     };
                     if (C::REST) {
-                        if (((p + 1 - S) & 1) == 0 && r >= a && r < b && keep &&
+                        if (((p + 1 - S) & 1) == 0 && rowin(r) && keep &&
                             (!G || (r >= 1 && r <= n - 2 && in0 && c0 <= n - 2))) {
                             const double res = rx();
-                            (rhsc + (long)(r >> 1) * pitchc)[c0 >> 1] = res;
+                            (rhsc + rowoff(r >> 1, ipc))[c0 >> 1] = res;
                         }
                     } else {
                         const double uE = dpp_shl1(ur[iR].x);
@@ -1056,13 +1062,13 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                                                ur[iS].y, uE, c);
                         };
                         if (!G) {   // acc + 0.0 == acc (acc >= +0): selects, no branch
-                            if (r >= a && r < b) {
+                            if (rowin(r)) {
                                 const double r0 = rx();
                                 const double r1 = ry();
                                 acc += keep ? r0 * r0 : 0.0;
                                 acc += keep ? r1 * r1 : 0.0;
                             }
-                        } else if (keep && r >= a && r < b && r >= 1 && r <= n - 1) {
+                        } else if (keep && rowin(r) && r >= 1 && r <= n - 1) {
                             if (in0) {
                                 const double res = rx();
                                 acc += res * res;
@@ -1252,6 +1258,10 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     const int nc = n >> 1;
     const double hh = c.h * 0.5;
     double acc = 0.0, acc2 = 0.0;
+    // row offsets as 32 x 32 -> 64-bit products (the pitches are < 2^31
+    // elements): two scalar multiplies per row address instead of a 64-bit one
+    const int ip = (int)pitch, ipc = (int)pitchc;
+    auto rowoff = [](int r, int p) { return (long)r * (long)p; };
 
     // One march of the pair over owned rows [a, b) of the strip whose lane 0
     // is column cb, owning columns [k0, k1) (G: see above; the unguarded form
@@ -1264,8 +1274,10 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
         // [ec0, ec1) are that launch's (one owner per output)
         const bool exc = G && c0 >= xg.ec0 && c0 < xg.ec1;
         const bool keep = act && c0 >= k0 && c0 < k1;
+        // (rows [a, b) as one unsigned compare: b >= a)
         auto own = [&](const int r) {
-            return r >= a && r < b && keep && !(exc && r >= xg.er0 && r < xg.er1);
+            return (unsigned)(r - a) < (unsigned)(b - a) && keep &&
+                   !(exc && r >= xg.er0 && r < xg.er1);
         };
         // XG: the neighbouring waves of this role (the outer waves' outer
         // edge lanes are halo: any value will do, their own slot)
@@ -1325,13 +1337,13 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
         // an even row needs only the coarse row below it)
         auto load_u = [&](int R, UPre &u, const bool odd) {
             const int Rc = min(max(R, lo), hi);
-            u.X = ld2u(uin + (long)Rc * pitch, bcl);
-            const double *p0 = uc + (long)(Rc >> 1) * pitchc;
+            u.X = ld2u(uin + rowoff(Rc, ip), bcl);
+            const double *p0 = uc + rowoff(Rc >> 1, ipc);
             u.q00 = ld1u(p0, bjl);
             u.q01 = ld1u(p0, bjl1);
             if (odd) {
-                u.q10 = ld1u(p0 + pitchc, bjl);
-                u.q11 = ld1u(p0 + pitchc, bjl1);
+                u.q10 = ld1u(p0 + ipc, bjl);
+                u.q11 = ld1u(p0 + ipc, bjl1);
             }
         };
         // + prolongation (gs.cpp:238-265); static parity, select (see k_wsmooth)
@@ -1365,12 +1377,12 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
         }
         auto load_rv = [&](int R, const int q) {
             const int Rc = min(max(R, lo), hi);
-            const long o = (long)Rc * pitch;
+            const long o = rowoff(Rc, ip);
             RowData &d = rd[q];
             d.r = ld2u(rhs + o, bcl);
-            if (SV) {
-                ar1[q] = sa1[Rc];
-                ar2[q] = sa2[Rc];
+            if (SV) {   // (32-bit byte offsets: the scalar loads' SGPR-offset form)
+                ar1[q] = *reinterpret_cast<const double *>(rowb(sa1, (unsigned)Rc * 8u));
+                ar2[q] = *reinterpret_cast<const double *>(rowb(sa2, (unsigned)Rc * 8u));
             } else {
                 const double2 x = ld2((v1 + o) + cl), y = ld2((v2 + o) + cl);
                 d.x = make_double2(x.x * hh, x.y * hh);
@@ -1518,7 +1530,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         const int ro = s + 2 - S;
                         const double2 uf = ur[(p + 2 - S + 2 * NR) % NR];
                         uring[pr][(p + 2 - S + 2 * NR) % NU][l] = uf;
-                        st2_ifu(upost + (long)ro * pitch, c0, post && own(ro),
+                        st2_ifu(upost + rowoff(ro, ip), c0, post && own(ro),
                                uf);
                     }
                     // residual norm of u_post (multigrid.cpp:112-113), column c0 of
@@ -1623,7 +1635,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         d.r = make_double2(f0, f1);
                         const bool i0 = !GN || (r >= 1 && r <= n - 1 && in0);
                         const bool i1 = !GN || (r >= 1 && r <= n - 1 && in1);
-                        double *row = rhs_next + (long)r * pitch;
+                        double *row = rhs_next + rowoff(r, ip);
                         if (own(r)) {
                             if (i0 && i1) {
                                 st2s(row + c0, d.r);
@@ -1644,7 +1656,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                     for (int h = 0; h < S; ++h) stage_c(q, h, s + 1 - h);
                     {
                         const int ro = s + 2 - S;
-                        st2_ifu(upre + (long)ro * pitch, c0, own(ro),
+                        st2_ifu(upre + rowoff(ro, ip), c0, own(ro),
                                ur[(q + 2 - S + 2 * NR) % NR]);
                     }
                     if (((q + 1 - S) & 1) == 0) {   // compile-time row parity
@@ -1657,7 +1669,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         const bool on = own(r) &&
                                         (!GN || (r >= 1 && r <= n - 2 && in0 && c0 <= n - 2));
                         const double res = res_x(iR, iN, iS, uW);
-                        st1_ifu(rhsc + (long)(r >> 1) * pitchc, c0 >> 1, on, res);
+                        st1_ifu(rhsc + rowoff(r >> 1, ipc), c0 >> 1, on, res);
                     }
                     post_edges(ur, q);
                     if (XG || (p & 1)) __syncthreads();
