@@ -41,7 +41,7 @@ long g_dist_min_rows = 256;
 // the coarse levels of the V-cycle (the level-0 pass that reads them waits
 // for it); 2 = that, and the cross pass's remaining exchange (level-1 u) on
 // the second stream too, beside the pass's interior march (the bands next to
-// the ghosts go to its edge launch); 0 (default) = every exchange on the
+// the ghosts go to its edge launch); 0 = every exchange on the
 // compute stream; -1 (default) = 1 on an RCCL communicator, 0 on virtual
 // ranks.  On virtual ranks (one GPU) the early exchange's copies compete with
 // the level passes for the same chip and cost 2-3 %; over xGMI it takes the
@@ -112,6 +112,10 @@ struct Dist {
     int la = 0;
     std::vector<Part> parts;   // local: `world` parts; RCCL: this rank's part
     ncclComm_t comm = nullptr;
+    // the side stream's exchanges (dist_overlap) run on their own communicator,
+    // split from `comm` (same ranks): NCCL operations of one communicator must
+    // not run concurrently from two streams, those of two communicators may
+    ncclComm_t comm_x = nullptr;
     double *hsum = nullptr;    // pinned
     // dist_overlap: ghost exchanges on a second stream beside the interior pass
     hipStream_t xs = nullptr;
@@ -146,6 +150,7 @@ void dist_free(mgx_ctx *c) {
         (void)hipFree(p.dsum);
         (void)hipFree(p.partials);
     }
+    if (d->comm_x) (void)ncclCommDestroy(d->comm_x);
     if (d->comm) (void)ncclCommDestroy(d->comm);
     if (d->xs) (void)hipStreamDestroy(d->xs);
     if (d->ev_fork) (void)hipEventDestroy(d->ev_fork);
@@ -247,6 +252,8 @@ static int exchange_rows(mgx_ctx *c, const std::vector<XF> &xs, hipStream_t st) 
         return MGX_OK;
     }
     Part &p = d->parts[0];
+    ncclComm_t comm = st == d->xs ? d->comm_x : d->comm;
+    if (!comm) return fail(MGX_E_INTERNAL, "ghost exchange: no communicator for this stream");
     ncclResult_t r = ncclGroupStart();
     for (const XF &x : xs) {
         PLevel &L = p.lv[x.l];
@@ -256,10 +263,10 @@ static int exchange_rows(mgx_ctx *c, const std::vector<XF> &xs, hipStream_t st) 
         for (const Xfer &t : plan) {
             if (r != ncclSuccess) break;
             r = ncclSend(a + (long)t.send_row * P, (size_t)t.send_rows * P, ncclDouble, t.peer,
-                         d->comm, st);
+                         comm, st);
             if (r == ncclSuccess)
                 r = ncclRecv(a + (long)t.recv_row * P, (size_t)t.recv_rows * P, ncclDouble,
-                             t.peer, d->comm, st);
+                             t.peer, comm, st);
         }
     }
     const ncclResult_t re = ncclGroupEnd();   // always close the group
@@ -549,14 +556,16 @@ static int dist_cross(mgx_ctx *c, bool store_post) {
     std::vector<XF> xl;
     if (!fresh) xl.push_back(XF{0, kU});
     if (1 < d->la) xl.push_back(XF{1, kU});
-    bool ov = overlap_mode(d) == 2 && d->world > 1 && !xl.empty();
+    // (the split launches are the unguarded kernel's: xfast on, d > 0)
+    bool ov = overlap_mode(d) == 2 && d->world > 1 && !xl.empty() && mgx::get_xfast() != 0;
     for (auto &p : d->parts) ov = ov && p.lv[0].rb - p.lv[0].ra >= 4 * G && p.lv[0].coef.dgs > 0;
     if (ov)
         CHK(side_exchange(c, xl, [] {}));
     else if (!xl.empty())
         CHK(xchg(c, xl));
-    // one launch (phase 1 / 2) or both of the pass over owned rows [ra, rb) of part p
-    auto pass = [&](Part &p, int P, int Q, int phase, int done) -> int {
+    // one launch (phase 1 / 2) or both of the pass over owned rows [ra, rb) of
+    // part p; an MGX status, the norm partials written in *blocks_out
+    auto pass = [&](Part &p, int P, int Q, int phase, int done, int *blocks_out) -> int {
         PLevel &L = p.lv[0];
         mgx::XArgs A;
         A.uin = L.U();
@@ -621,7 +630,8 @@ static int dist_cross(mgx_ctx *c, bool store_post) {
             }
         }
         if (blocks < 0) return fail(MGX_E_ARG, "launch_xsmooth: unsupported sweeps / block");
-        return blocks;
+        *blocks_out = blocks;
+        return MGX_OK;
     };
     std::vector<std::pair<int, int>> bufs;
     for (auto &p : d->parts) {
@@ -633,19 +643,17 @@ static int dist_cross(mgx_ctx *c, bool store_post) {
     }
     if (!ov) {
         for (size_t i = 0; i < d->parts.size(); ++i) {
-            const int r = pass(d->parts[i], bufs[i].first, bufs[i].second, 0, 0);
-            if (r < 0) return r;
+            int blocks = 0;
+            CHK(pass(d->parts[i], bufs[i].first, bufs[i].second, 0, 0, &blocks));
         }
     } else {
-        std::vector<int> done(d->parts.size());
-        for (size_t i = 0; i < d->parts.size(); ++i) {
-            done[i] = pass(d->parts[i], bufs[i].first, bufs[i].second, 1, 0);
-            if (done[i] < 0) return done[i];
-        }
+        std::vector<int> done(d->parts.size(), 0);
+        for (size_t i = 0; i < d->parts.size(); ++i)
+            CHK(pass(d->parts[i], bufs[i].first, bufs[i].second, 1, 0, &done[i]));
         HIPCHK(hipStreamWaitEvent(c->stream, d->ev_join, 0));
         for (size_t i = 0; i < d->parts.size(); ++i) {
-            const int r = pass(d->parts[i], bufs[i].first, bufs[i].second, 2, done[i]);
-            if (r < 0) return r;
+            int blocks = 0;
+            CHK(pass(d->parts[i], bufs[i].first, bufs[i].second, 2, done[i], &blocks));
         }
     }
     for (size_t i = 0; i < d->parts.size(); ++i) {
@@ -1202,6 +1210,12 @@ int mgx_create_dist(mgx_ctx **out, long n, int maxlvl, double dt, double nu,
         if (r != ncclSuccess) {
             free_ctx(c);
             return fail(MGX_E_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+        }
+        // the side stream's communicator (collective: every rank splits here)
+        r = ncclCommSplit(c->dist->comm, 0, rank, &c->dist->comm_x, nullptr);
+        if (r != ncclSuccess) {
+            free_ctx(c);
+            return fail(MGX_E_RCCL, std::string("ncclCommSplit: ") + ncclGetErrorString(r));
         }
     }
     int rc = build_dist(c, world, {rank});

@@ -1,7 +1,7 @@
 // fake_rccl.hip -- TEST INFRASTRUCTURE ONLY (never linked into libmgx.so).
 //
 // An in-process stand-in for exactly the RCCL entry points dist.hip calls:
-// ncclGetUniqueId, ncclCommInitRank / ncclCommDestroy, ncclGroupStart /
+// ncclGetUniqueId, ncclCommInitRank / ncclCommSplit / ncclCommDestroy, ncclGroupStart /
 // ncclGroupEnd, ncclSend / ncclRecv, ncclAllGather, ncclAllReduce (sum),
 // ncclBroadcast, ncclGetErrorString.  Ranks are host THREADS of one process,
 // all on one GPU, so libmgx's real RCCL code path (dist.hip, the branch a
@@ -44,10 +44,11 @@
 namespace fk {
 
 enum Fn { kInit, kDestroy, kGroupStart, kGroupEnd, kSend, kRecv, kAllGather, kAllReduce,
-          kBroadcast, kUniqueId, kNumFn };
+          kBroadcast, kUniqueId, kSplit, kNumFn };
 const char *kFnNames[kNumFn] = {"ncclCommInitRank", "ncclCommDestroy", "ncclGroupStart",
                                 "ncclGroupEnd", "ncclSend", "ncclRecv", "ncclAllGather",
-                                "ncclAllReduce", "ncclBroadcast", "ncclGetUniqueId"};
+                                "ncclAllReduce", "ncclBroadcast", "ncclGetUniqueId",
+                                "ncclCommSplit"};
 std::atomic<long> g_calls[kNumFn];
 std::atomic<long> g_bytes{0};
 std::mutex g_err_mu;
@@ -133,6 +134,7 @@ struct ncclComm {
     std::string key;
     int rank = 0, world = 0;
     long seq = 0;                      // collectives issued by this rank
+    long splits = 0;                   // ncclCommSplit calls by this rank
     std::vector<hipEvent_t> events;    // destroyed with the communicator
     double *stage = nullptr;           // all-reduce staging (this rank's stream only)
     size_t stage_bytes = 0;
@@ -399,11 +401,7 @@ ncclResult_t ncclGetUniqueId(ncclUniqueId *id) {
     return ncclSuccess;
 }
 
-ncclResult_t ncclCommInitRank(ncclComm_t *out, int nranks, ncclUniqueId id, int rank) {
-    g_calls[kInit]++;
-    if (!out || nranks < 1 || rank < 0 || rank >= nranks)
-        return bad(ncclInvalidArgument, "ncclCommInitRank: bad args");
-    const std::string key(id.internal, sizeof(id.internal));
+static ncclResult_t init_rank(ncclComm_t *out, int nranks, const std::string &key, int rank) {
     std::shared_ptr<Clique> q;
     {
         std::lock_guard<std::mutex> g(g_mu);
@@ -446,6 +444,28 @@ ncclResult_t ncclCommInitRank(ncclComm_t *out, int nranks, ncclUniqueId id, int 
     }
     *out = c;
     return ncclSuccess;
+}
+
+ncclResult_t ncclCommInitRank(ncclComm_t *out, int nranks, ncclUniqueId id, int rank) {
+    g_calls[kInit]++;
+    if (!out || nranks < 1 || rank < 0 || rank >= nranks)
+        return bad(ncclInvalidArgument, "ncclCommInitRank: bad args");
+    return init_rank(out, nranks, std::string(id.internal, sizeof(id.internal)), rank);
+}
+
+// Only the split libmgx makes: every rank the same colour, key = its rank, so
+// the new communicator has the parent's ranks (a fresh clique: its own
+// mailboxes and collective sequence, as a separate NCCL communicator has).
+// The k-th split of a parent on every rank joins the same clique.
+ncclResult_t ncclCommSplit(ncclComm_t comm, int color, int key, ncclComm_t *out,
+                           ncclConfig_t *config) {
+    g_calls[kSplit]++;
+    (void)config;
+    if (!comm || !out) return bad(ncclInvalidArgument, "ncclCommSplit: bad args");
+    if (color != 0 || key != comm->rank)
+        return bad(ncclInvalidArgument, "ncclCommSplit: only colour 0 with key = rank is faked");
+    const std::string k = comm->key + "/split" + std::to_string(comm->splits++);
+    return init_rank(out, comm->world, k, comm->rank);
 }
 
 ncclResult_t ncclCommDestroy(ncclComm_t c) {
