@@ -50,42 +50,51 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s HBM3E
-# (kind, level) -> kernel (template instance) of the default config, for the
-# PMC traffic summary committed under profiles/ (tools/profile_round.sh)
-# (the cross pass is two launches: the unguarded interior kernel and the
-# guarded edge kernel; their traffic is summed)
-KERNEL_IDS = {(8, 0): ("mgx::k_xsmooth<4, 3, false, false, true, false>",
-                       "mgx::k_xsmooth<1, 3, true, false, true, false>"),
-              (0, 0): ("mgx::k_wsmooth<4, 3, 4, true>",),
-              (7, 0): ("mgx::k_wsmooth<4, 3, 10, true>",)}
-KERNELS_HIP = os.path.join(ROOT, "hpcclassmultigridproject_amd", "csrc", "kernels.hip")
+# kernel (template instances) of the dominant pass of the default config per
+# fp_mode, for the PMC traffic summary committed under profiles/
+# (tools/profile_round.sh): the cross pass is two launches, the unguarded
+# interior kernel and the guarded edge kernel; their traffic is summed.
+# k_xsmooth<WPB, K, G, RS, SV, FM>
+KERNEL_IDS = {("fma", 8): ("mgx::k_xsmooth<4, 3, false, false, true, true>",
+                           "mgx::k_xsmooth<1, 3, true, false, true, true>"),
+              ("bitwise", 8): ("mgx::k_xsmooth<4, 3, false, false, true, false>",
+                               "mgx::k_xsmooth<1, 3, true, false, true, false>"),
+              ("fma-generic", 8): ("mgx::k_xsmooth<4, 3, false, false, false, true>",
+                                   "mgx::k_xsmooth<1, 3, true, false, false, true>")}
+CSRC = os.path.join(ROOT, "hpcclassmultigridproject_amd", "csrc")
+KERNEL_SOURCES = ("stencil.h", "kernels.h", "kernels.hip", "wsmooth.hip", "xsmooth.hip")
 
 
 def kernels_sha():
+    """sha256 of the stencil kernel sources (a PMC profile is reused only while
+    they are unchanged)."""
     import hashlib
-    return hashlib.sha256(open(KERNELS_HIP, "rb").read()).hexdigest()
+    h = hashlib.sha256()
+    for f in KERNEL_SOURCES:
+        h.update(open(os.path.join(CSRC, f), "rb").read())
+    return h.hexdigest()
 
 
-def traffic_profile():
+def traffic_profile(mode):
     """(path, kernels) of the newest profiles/*_hbm_traffic.json collected from
-    the kernels.hip that is built now, or (None, reason)."""
+    the kernel sources built now in fp mode `mode`, or (None, reason)."""
     import glob
     sha = kernels_sha()
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_hbm_traffic.json")),
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*hbm_traffic*.json")),
                    key=os.path.getmtime, reverse=True)
     for f in files:
         d = json.load(open(f))
-        if d.get("kernels_hip_sha256") == sha:
+        if d.get("kernel_sources_sha256") == sha and d.get("mode") == mode:
             return os.path.relpath(f, ROOT), d["kernels"]
-    return None, (f"no profiles/*_hbm_traffic.json matches kernels.hip sha256 {sha[:12]} "
-                  "(regenerate with tools/profile_round.sh)")
+    return None, (f"no profiles/*_hbm_traffic.json ({mode}) matches the kernel sources' sha256 "
+                  f"{sha[:12]} (regenerate with tools/profile_round.sh)")
 
 
-def lookup_traffic(knames, field="hbm_bytes"):
+def lookup_traffic(knames, mode, field="hbm_bytes"):
     """HBM bytes (or another per-dispatch PMC field) of the finest-level
     instances (largest traffic) of the kernels in knames, summed (one launch of
     the op = one dispatch of each)."""
-    path, kernels = traffic_profile()
+    path, kernels = traffic_profile(mode)
     if path is None:
         return None, None, kernels
     keys, total = [], 0.0
@@ -127,8 +136,14 @@ def parse():
                          "in the warm-up (3 cycles each, max over ranks) and keep the fastest")
     ap.add_argument("--rccl-check", type=int, default=1,
                     help="N > 1: first check libmgx's RCCL path bitwise vs one GPU (N=4096)")
-    ap.add_argument("--no-generic", action="store_true",
-                    help="skip the comparison run with the generic (2-D) velocity path")
+    ap.add_argument("--fp-mode", choices=["fma", "bitwise"], default="fma",
+                    help="arithmetic of the smoothing passes (mgx_options.fp_mode): fma = "
+                         "contracted, within 1e-12 of the reference; bitwise = the reference's "
+                         "bits")
+    ap.add_argument("--reps", type=int, default=5,
+                    help="timed repetitions of --steps cycles; value = the median (SURVEY 8d)")
+    ap.add_argument("--no-compare", "--no-generic", action="store_true", dest="no_compare",
+                    help="skip the comparison runs (other fp_mode, generic velocity path)")
     ap.add_argument("--no-profile", action="store_true",
                     help="do not record per-kernel HIP events in the timed region")
     ap.add_argument("--sweep", nargs=2, type=int, metavar=("NMIN", "NMAX"),
@@ -295,6 +310,7 @@ def main():
             N, L, g = 2 * N, L + 1, 4 * g
     nu = -4e-4
     dt = 1.0 / N / 10
+    fp = _lib.FP_FMA if args.fp_mode == "fma" else _lib.FP_BITWISE
     dist_kw = {}
     if world > 1:
         from hpcclassmultigridproject_amd import dist as mgdist
@@ -310,7 +326,8 @@ def main():
     tower = (pkg._lib.TOWER_CORRECT if row_upload or N > 16384
              else pkg._lib.TOWER_REFERENCE)
     mg = pkg.Multigrid(N, L, dt, nu, nsmooth=args.nsmooth, device=local,
-                       smoother=args.smoother, fuse=args.fuse, tower_mode=tower, **dist_kw)
+                       smoother=args.smoother, fuse=args.fuse, tower_mode=tower, fp_mode=fp,
+                       **dist_kw)
     la = mg.dist_info()[2]
     if row_upload:
         lo, hi = mg.dist_rows(0)
@@ -335,10 +352,15 @@ def main():
     if world > 1:
         # price the exchange schedules on this machine (untimed warm-up): the
         # early level-0 exchange behind the coarse levels pays over xGMI but not
-        # on one GPU's virtual ranks
+        # on one GPU's virtual ranks; a schedule whose
+        # RCCL self-check was not bitwise is not a candidate
+        ok_modes = [0, 1, 2]
+        if rccl_check is not None and isinstance(rccl_check.get("modes"), dict):
+            ok_modes = [m for m in ok_modes
+                        if rccl_check["modes"].get(str(m), {}).get("bitwise", False)] or [0]
         if args.overlap == "auto":
             overlap_ab = {}
-            for ov in (0, 1, 2):
+            for ov in ok_modes:
                 _lib.set_tuning("dist_overlap", ov)
                 mg.run_cycles(1)
                 mg.synchronize()
@@ -353,30 +375,44 @@ def main():
         _lib.set_tuning("dist_overlap", best_ov)
         mg.run_cycles(1)
         mg.synchronize()
-    mg.profile_reset()
-    if not args.no_profile:
-        # HIP events around the finest-level launches only (the dominant
-        # kernels); events around every small-level launch would cost ~7%
-        mg.profile(True, finest_only=True)
 
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    # K steps = K V-cycles, each followed by its residual norm (read back per
-    # cycle, as mg_outer does); the solution after the K-th is materialised
-    res = mg.run_cycles(args.steps)
-    mg.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    elapsed = max_over_ranks(time.perf_counter() - t0)
+    def timed_reps(m, reps, prof):
+        """SURVEY 8(d) protocol: `reps` repetitions of K cycles, each bracketed
+        by barrier + synchronize, max over ranks; HIP events around the
+        finest-level launches (prof); -> (seconds per repetition, residual)."""
+        m.profile_reset()
+        if prof:
+            # events around the finest-level launches only (the dominant
+            # kernels); events around every small-level launch would cost ~7%
+            m.profile(True, finest_only=True)
+        secs, res = [], None
+        for _ in range(reps):
+            barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            # K steps = K V-cycles, each followed by its residual norm (read
+            # back per cycle, as mg_outer does); the K-th cycle's solution is
+            # materialised
+            res = m.run_cycles(args.steps)
+            m.synchronize()
+            barrier()
+            torch.cuda.synchronize()
+            secs.append(max_over_ranks(time.perf_counter() - t0))
+        return secs, res
 
-    # dominant kernel = the finest-level (kind) with the largest device time
-    # in the timed region
-    best = None
-    for kind in _lib.KERNEL_NAMES:
-        n, ms, b, cb = mg.profile_get_ex(kind, 0)
-        if n and (best is None or ms > best[3]):
-            best = (kind, 0, n, ms, b, cb)
+    def dominant(m):
+        """(kind, level 0, launches, ms, canonical bytes, compulsory bytes) of
+        the finest-level kernel with the largest device time since the reset."""
+        best = None
+        for kind in _lib.KERNEL_NAMES:
+            n, ms, b, cb = m.profile_get_ex(kind, 0)
+            if n and (best is None or ms > best[3]):
+                best = (kind, 0, n, ms, b, cb)
+        return best
+
+    rep_s, res = timed_reps(mg, args.reps, not args.no_profile)
+    elapsed = sorted(rep_s)[len(rep_s) // 2]   # the median repetition
+    best = dominant(mg)
     mg.profile(False)
 
     # per-kernel, per-level breakdown: a few more cycles, every launch timed
@@ -407,81 +443,106 @@ def main():
         _lib.check(_lib.lib().mgx_velocity_factored(mg.handle, ctypes.byref(fac)))
     mg.close()
 
-    # the same V-cycle with the generic velocity path (2-D v1 / v2 on every
-    # row of every level: sep_velocity = zero_rows = 0), for comparison: the
-    # headline reads the reference flow's exact rank-1 factors on level 0 and
-    # skips the coarse levels' all-zero velocity rows
-    generic = None
-    if world == 1 and not args.no_generic:
-        keys = {k: _lib.get_tuning(k) for k in ("sep_velocity", "zero_rows")}
+    def roofline(best, mode, v_extra=0.0):
+        """Roofline of the dominant kernel: achieved = its compulsory bytes per
+        launch (each array the fused pass must read or write, once) / its live
+        mean event duration; v_extra: bytes of the 2-D velocity arrays the pass
+        reads on the generic path (already in its compulsory bytes there)."""
+        kind, lvl, n0, ms0, b0, cb0 = best
+        per_launch = cb0 / n0
+        avg_s = ms0 * 1e-3 / n0
+        achieved = per_launch / avg_s / 1e9
+        r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+             "kernel": f"{_lib.KERNEL_NAMES[kind]} level {lvl}",
+             "compulsory_bytes_per_launch": per_launch,
+             "avg_launch_ms": round(avg_s * 1e3, 4),
+             "launches": n0,
+             "canonical_bytes_per_launch": b0 / n0,
+             "canonical_equiv_GBs": round(b0 / n0 / avg_s / 1e9, 1)}
+        # the committed PMC traffic is per launch of the single-GPU pass; a
+        # rank's row block moves a fraction of it, so it is not reused there
+        ids = KERNEL_IDS.get((mode, kind)) if (N, L, args.nsmooth, args.smoother, args.fuse,
+                                                world) == (16384, 9, 3, 0, 3, 1) else None
+        if not ids:
+            r["traffic_null_reason"] = "no committed PMC profile for this configuration"
+            return r
+        kname, traffic, tsrc = lookup_traffic(ids, mode)
+        if not traffic:
+            r["traffic_null_reason"] = tsrc
+            return r
+        r["kernel"] += f" = {kname}"
+        r["traffic"] = traffic
+        r["traffic_source"] = tsrc
+        # measured HBM bytes (rocprofv3 PMC, profiles/) / live mean duration
+        r["hbm_GBs"] = round(traffic / avg_s / 1e9, 1)
+        r["hbm_frac"] = round(traffic / avg_s / 1e9 / HBM_PEAK_GBS, 4)
+        r["traffic_over_compulsory"] = round(traffic / per_launch, 3)
+        # the profile's own kernel durations (rocprofv3, sum of the pass's
+        # launches): the live event mean should agree with them
+        _, pms, _ = lookup_traffic(ids, mode, "ms_profiled")
+        if pms:
+            r["profiled_launch_ms"] = round(pms, 4)
+            r["live_over_profiled"] = round(avg_s * 1e3 / pms, 4)
+        # VALU wave-instructions per launch (PMC SQ_INSTS_VALU, same profile)
+        # against the issue capacity of the live duration (one wave64
+        # instruction per 4 cycles per SIMD, 1024 SIMDs, 2.4 GHz peak clock:
+        # a lower bound on the busy fraction)
+        _, valu, _ = lookup_traffic(ids, mode, "SQ_INSTS_VALU")
+        if valu:
+            cap = 1024 * avg_s * 2.4e9 / 4
+            r["valu"] = {"insts_per_launch": valu, "issue_capacity": round(cap),
+                         "issue_frac": round(valu / cap, 4),
+                         "note": "VALU wave-instructions / (1024 SIMDs x 2.4 GHz / 4 "
+                                 "cycles per wave64 op x live mean duration)"}
+        return r
+
+    def side_run(label, fpm, tuning, reps):
+        """The same workload in another configuration (one GPU): fp_mode fpm
+        and process tuning keys `tuning`, `reps` repetitions of K cycles."""
+        keys = {k: _lib.get_tuning(k) for k in tuning}
         try:
-            for k in keys:
-                _lib.set_tuning(k, 0)
+            for k, v in tuning.items():
+                _lib.set_tuning(k, v)
             g = pkg.Multigrid(N, L, dt, nu, nsmooth=args.nsmooth, device=local,
-                              smoother=args.smoother, fuse=args.fuse, tower_mode=tower)
+                              smoother=args.smoother, fuse=args.fuse, tower_mode=tower,
+                              fp_mode=fpm)
             u0, v1, v2 = pkg.init_problem(N, nthreads=16)
             g.upload(u0, v1, v2)
             del u0, v1, v2
             g.rhs()
             g.run_cycles(2)
             g.synchronize()
-            t0 = time.perf_counter()
-            g.run_cycles(args.steps)
-            g.synchronize()
-            gms = (time.perf_counter() - t0) / args.steps * 1e3
+            secs, _ = timed_reps(g, reps, True)
+            b = dominant(g)
+            g.profile(False)
             g.close()
-            generic = {"ms_per_step": round(gms, 4),
-                       "value": (N - 1) ** 2 / (gms * 1e-3),
-                       "note": "sep_velocity=0, zero_rows=0: every velocity row read from HBM"}
         finally:
             for k, v in keys.items():
                 _lib.set_tuning(k, v)
+        med = sorted(secs)[len(secs) // 2]
+        mode = ("fma" if fpm == _lib.FP_FMA else "bitwise") + \
+               ("-generic" if tuning.get("sep_velocity") == 0 else "")
+        return {"label": label, "ms_per_step": round(med / args.steps * 1e3, 4),
+                "rep_ms_per_step": [round(x / args.steps * 1e3, 4) for x in secs],
+                "value": (N - 1) ** 2 * args.steps / med,
+                "roofline": roofline(b, mode) if b else None}
 
-    roof = None
-    if best:
-        kind, lvl, n0, ms0, b0, cb0 = best
-        # achieved = compulsory bytes per launch (each array the fused pass must
-        # read or write, once) / live mean duration; the per-op canonical bytes
-        #  of the reference ops it replaces go in canonical_equiv_GBs
-        per_launch = cb0 / n0
-        avg_s = ms0 * 1e-3 / n0
-        achieved = per_launch / avg_s / 1e9
-        # the committed PMC traffic is per launch of the single-GPU pass; a
-        # rank's row block moves a fraction of it, so it is not reused there
-        ids = KERNEL_IDS.get((kind, lvl)) if (N, L, args.nsmooth, args.smoother, args.fuse,
-                                              world) == (16384, 9, 3, 0, 3, 1) else None
-        kname, traffic, tsrc = (None, None, "no committed PMC profile for this configuration")
-        if ids:
-            kname, traffic, tsrc = lookup_traffic(ids)
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": f"{_lib.KERNEL_NAMES[kind]} level {lvl}"
-                          + (f" = {kname}" if kname else ""),
-                "compulsory_bytes_per_launch": per_launch,
-                "avg_launch_ms": round(avg_s * 1e3, 4),
-                "canonical_bytes_per_launch": b0 / n0,
-                "canonical_equiv_GBs": round(b0 / n0 / avg_s / 1e9, 1)}
-        if traffic:
-            # measured HBM bytes (rocprofv3 PMC, profiles/) / live mean duration
-            roof["traffic_source"] = tsrc
-            roof["hbm_GBs"] = round(traffic / avg_s / 1e9, 1)
-            roof["hbm_frac"] = round(traffic / avg_s / 1e9 / HBM_PEAK_GBS, 4)
-            roof["traffic_over_compulsory"] = round(traffic / per_launch, 3)
-            # the pass is bound by its instruction stream more than by bytes:
-            # VALU instructions per launch (PMC SQ_INSTS_VALU, same profile)
-            # against the issue capacity in its live duration (one wave
-            # instruction per 4 cycles per SIMD, 1024 SIMDs, 2.4 GHz peak clock:
-            # a lower bound on the busy fraction)
-            _, valu, _ = lookup_traffic(ids, "SQ_INSTS_VALU")
-            if valu:
-                cap = 1024 * avg_s * 2.4e9 / 4
-                roof["valu"] = {"insts_per_launch": valu, "issue_capacity": round(cap),
-                                "issue_frac": round(valu / cap, 4),
-                                "note": "VALU wave-instructions / (1024 SIMDs x 2.4 GHz / 4 "
-                                        "cycles per wave64 op x live mean duration)"}
-        else:
-            roof["traffic_null_reason"] = tsrc
+    fp_name = "fma" if fp == _lib.FP_FMA else "bitwise"
+    other = None
+    generic = None
+    if world == 1 and not args.no_compare:
+        # the other arithmetic mode (bitwise: every value the reference's)
+        ofp = _lib.FP_BITWISE if fp == _lib.FP_FMA else _lib.FP_FMA
+        other = side_run("bitwise" if ofp == _lib.FP_BITWISE else "fma", ofp, {}, 3)
+        # the generic velocity path (2-D v1 / v2 on every row of every level:
+        # sep_velocity = zero_rows = 0): the headline reads the reference
+        # flow's exact rank-1 factors on level 0 and skips the coarse levels'
+        # all-zero velocity rows (DESIGN.md section 4)
+        generic = side_run("generic velocity", fp, {"sep_velocity": 0, "zero_rows": 0}, 3)
+        generic["note"] = "sep_velocity=0, zero_rows=0: every velocity row read from HBM"
 
+    roof = roofline(best, fp_name) if best else None
     value = (N - 1) ** 2 * args.steps / elapsed
     # SURVEY 8d secondary metric: RB-GS point updates per second
     smoother_pts = sum(2 * args.nsmooth * ((N >> l) - 1) ** 2 for l in range(L - 1))
@@ -505,11 +566,17 @@ def main():
             "GBs": round(a2, 1), "frac": round(a2 / HBM_PEAK_GBS, 4),
             "note": "compulsory bytes with v1, v2 counted as read (they are regenerated "
                     "bitwise from their rank-1 factors instead)"}
+    reps_ms = [x / args.steps * 1e3 for x in rep_s]
     out = {
         "metric": f"V-cycle grid-point-updates/sec at N={N}; achieved HBM GB/s vs peak",
         "value": value, "unit": "grid-point-updates/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "reps": len(rep_s), "median": value,
+        "rep_ms_per_step": [round(x, 4) for x in reps_ms],
+        "spread": {"min_ms_per_step": round(min(reps_ms), 4),
+                   "max_ms_per_step": round(max(reps_ms), 4),
+                   "rel": round((max(reps_ms) - min(reps_ms)) / (elapsed / args.steps * 1e3), 4)},
         "smoother_point_updates_per_s": smoother_pts * args.steps / elapsed,
         "scaling": "single" if world == 1 else ("weak" if args.weak else "strong"),
         "vs_baseline": None, "dtype": "f64",
@@ -518,6 +585,15 @@ def main():
         "config": {"workload": f"N={N} fp64 V-cycle, L={L} (coarsest {N >> (L - 1)}), "
                                f"nu_smooth={args.nsmooth}, + residual/norm per step",
                    "N": N, "levels": L, "nsmooth": args.nsmooth,
+                   "fp_mode": fp_name,
+                   "parity": ("fma: contracted smoothing passes, max|duT| <= 1e-12 vs the "
+                              "reference with identical cycle counts (tests/test_gpu_fma.py)"
+                              if fp == _lib.FP_FMA else
+                              "bitwise: u equal to the reference bit for bit "
+                              "(tests/test_gpu_solver.py sha256)"),
+                   "protocol": f"{args.warmup} warm-up cycles, then {len(rep_s)} repetitions "
+                               f"of {args.steps} timed cycles; value = the median repetition "
+                               "(SURVEY 8(d))",
                    "tower": ("correct (row-block upload)" if row_upload else
                              "correct" if tower == pkg._lib.TOWER_CORRECT else "reference"),
                    "parallelism": (f"row-partition x{world} on levels 0..{la - 1}, "
@@ -531,6 +607,7 @@ def main():
         "velocity": ("level 0: exact rank-1 factors (sep_velocity); coarse levels: all-zero "
                      "rows from one L2-resident row (zero_rows)" if fac.value else
                      "2-D arrays"),
+        "other_fp_mode": other,
         "generic_velocity_path": generic,
     }
     if rccl_check is not None:

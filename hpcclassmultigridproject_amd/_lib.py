@@ -16,6 +16,7 @@ HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "mgx.h")
 
 MGX_OK, MGX_E_ARG, MGX_E_HIP, MGX_E_RCCL, MGX_E_NOCONV = 0, 1, 2, 3, 4
 TOWER_REFERENCE, TOWER_CORRECT = 0, 1
+FP_BITWISE, FP_FMA = 0, 1   # mgx_options.fp_mode
 UNIQUE_ID_BYTES = 128   # MGX_UNIQUE_ID_BYTES (ncclUniqueId)
 K_GS, K_RESTRICT, K_PROLONG, K_RESNORM, K_COARSE, K_RHS, K_HALO, K_PSMOOTH, K_XSMOOTH = range(9)
 KERNEL_NAMES = {K_GS: "gs_sweep", K_RESTRICT: "residual_restrict", K_PROLONG: "prolong_add",
@@ -34,7 +35,8 @@ class Options(C.Structure):
     """mgx_options (include/mgx.h)."""
     _fields_ = [("nsmooth", C.c_int), ("shape", C.c_int), ("tower_mode", C.c_int),
                 ("device", C.c_int), ("coarse_tol", C.c_double), ("coarse_maxit", C.c_int),
-                ("max_cycle", C.c_int), ("smoother", C.c_int), ("fuse", C.c_int)]
+                ("max_cycle", C.c_int), ("smoother", C.c_int), ("fuse", C.c_int),
+                ("fp_mode", C.c_int)]
 
 
 _dp = C.POINTER(C.c_double)

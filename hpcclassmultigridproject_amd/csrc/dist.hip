@@ -182,7 +182,7 @@ static int build_dist(mgx_ctx *c, int world, const std::vector<int> &ranks) {
             PLevel L;
             L.n = c->N >> l;
             L.pitch = mgx::tower_pitch(L.n);
-            L.coef = mgx::make_coef(c->dt, c->nu, h);
+            L.coef = mgx::make_coef(c->dt, c->nu, h, c->opt.fp_mode == MGX_FP_FMA);
             alloc_rows(c->N, l, world, r, &L.ra, &L.rb, &L.lo, &L.hi);
             const bool third = l == 0 && L.n >= kCrossMinN;
             double **bufs[6] = {&L.u[0], &L.u[1], &L.rhs, &L.v1, &L.v2, &L.u[2]};
@@ -522,7 +522,7 @@ static int coarse_cycle(mgx_ctx *c, int l) {
 static bool dist_cross_ok(mgx_ctx *c) {
     Dist *d = c->dist;
     return cross_cycle_on() && d->la >= 1 && d->parts[0].lv[0].u[2] &&
-           c->opt.smoother == 0 && c->opt.shape == 1 &&
+           c->opt.smoother == 0 && c->opt.shape >= 1 &&
            (c->opt.nsmooth == 2 || c->opt.nsmooth == 3) && c->opt.fuse >= c->opt.nsmooth;
 }
 
@@ -712,6 +712,16 @@ int dist_vcycle(mgx_ctx *c, double *norm, bool store_post) {
             CHK(smooth(c, 0, false, /*restrict=*/true, false));
             CHK(coarse_rhs_ready(c, 0));
             CHK(early_u0(c, d->parts[0].lv[0].cur));
+        }
+        // W-cycles: visit sh's post- and visit sh+1's pre-smoothing as one
+        // cross pass (mgx.hip:op_vcycle)
+        for (int sh = 1; sh < c->opt.shape; ++sh) {
+            CHK(coarse_cycle(c, 1));
+            CHK(dist_cross(c, /*store_post=*/false));
+            for (auto &p : d->parts) {
+                p.lv[0].cur = p.lv[0].spec;
+                p.lv[0].spec = -1;
+            }
         }
         CHK(coarse_cycle(c, 1));
         if (c->post_only) {   // mg_outer's last cycle: post-smoothing + norm only

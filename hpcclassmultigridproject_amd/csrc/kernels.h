@@ -17,10 +17,15 @@ namespace mgx {
 struct Coef {
     double rr, nu, h, dgs, drhs, rdgs;   // rdgs = RN(1/dgs)
     unsigned dsign;                       // sign bit of dgs (high-word position)
+    // fp_mode fma (MGX_FP_FMA): the operator divided by its diagonal, see
+    // stencil.h "fp_mode fma".  g = rr/d, gn = g*nu.
+    double g, gn;
+    int fm;   // 1: the smoothing passes run the contracted (fma) forms
 };
-Coef make_coef(double k, double nu, double h);
+// fm: the context's fp_mode (0 bitwise, 1 fma)
+Coef make_coef(double k, double nu, double h, int fm = 0);
 
-// (+ MGX_PITCH_PAD extra doubles, a multiple of 16: row-pitch experiments)
+// row pitch of the tower layout: n+1 rounded up to 16 doubles (128 B)
 long tower_pitch(long n);
 
 // ---------------------------------------------------------------- reference layout
@@ -139,11 +144,6 @@ bool xstep_supported(long n);
 // Cross pass: 1 = interior strips run the unguarded march (default), 0 = all guarded.
 void set_xfast(long v);
 long get_xfast();
-// Cross pass interior kernel: 1 = the group-exchange form (a workgroup's strips
-// adjacent, edge columns through LDS: 28 halo columns per 512), 0 (default) =
-// separate strips with their own halos (28 per 128).  Bitwise the same.
-void set_xgroup(long v);
-long get_xgroup();
 void set_march_tile_rows(long v);
 long get_march_tile_rows();
 // Cross pass on row blocks of <= xtile_max_rows rows (default 4097): edges as
@@ -151,8 +151,7 @@ long get_march_tile_rows();
 void set_xtile_max_rows(long v);
 long get_xtile_max_rows();
 // Levels with n <= tile_max_n use the 2-D tile form of the fused pass (small
-// levels: latency bound), larger ones the row march.  Default 2048, or the
-// MGX_TILE_MAX_N environment variable.
+// levels: latency bound), larger ones the row march.  Default 1024.
 void set_tile_max_n(long v);
 long get_tile_max_n();
 // K = 3 tile passes on levels n >= tile32_min_n use 32 x 64 output tiles

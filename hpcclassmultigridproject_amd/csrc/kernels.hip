@@ -15,17 +15,10 @@
 
 namespace mgx {
 
-long tower_pitch(long n) {
-    static long pad = -1;
-    if (pad < 0) {
-        const char *e = getenv("MGX_PITCH_PAD");
-        pad = e ? std::max(0L, atol(e) / 16 * 16) : 0;
-    }
-    return (n + 1 + 15) / 16 * 16 + pad;
-}
+long tower_pitch(long n) { return (n + 1 + 15) / 16 * 16; }
 
-Coef make_coef(double k, double nu, double h) {
-    Coef c;
+Coef make_coef(double k, double nu, double h, int fm) {
+    Coef c{};
     c.rr = 0.5 * k / (h * h);            // gs.cpp:9-11
     c.nu = nu;
     c.h = h;
@@ -33,6 +26,9 @@ Coef make_coef(double k, double nu, double h) {
     c.drhs = 1.0 + 4.0 * c.rr * nu;      // gs.cpp:44
     c.rdgs = 1.0 / c.dgs;                // RN(1/d) for the Markstein division
     c.dsign = std::signbit(c.dgs) ? 0x80000000u : 0u;
+    c.g = c.rr / c.dgs;
+    c.gn = c.g * nu;
+    c.fm = fm ? 1 : 0;
     return c;
 }
 
@@ -503,6 +499,8 @@ __global__ __launch_bounds__(256) void k_prolong_add(double *uf, long pitchf,
 }
 
 // Coarsest level in one workgroup (multigrid.cpp:55-65), in place.
+// FM: fp_mode fma (stencil.h): the contracted update and residual.
+template <bool FM>
 __global__ __launch_bounds__(1024) void k_coarse_solve(double *u, const double *rhs,
                                                        const double *v1, const double *v2,
                                                        int n, long pitch, Coef c, double tol,
@@ -514,6 +512,7 @@ __global__ __launch_bounds__(1024) void k_coarse_solve(double *u, const double *
     // 64 x 16 threads: lane tx walks the columns, ty the rows (no integer
     // division in the loops: 64-bit div/mod is a long emulated sequence)
     const int tx = t & 63, ty = t >> 6;
+    const double hh = c.h * 0.5;   // FM: t = v*h/2
     if (zero_first) {
         for (long p = t; p < (long)(n + 1) * pitch; p += 1024) u[p] = 0.0;
         __syncthreads();
@@ -527,8 +526,10 @@ __global__ __launch_bounds__(1024) void k_coarse_solve(double *u, const double *
                 const int jc = 1 + ((i + 1 + colour) & 1);
                 for (int j = jc + 2 * tx; j <= n - 1; j += 128) {
                     const long p = (long)i * pitch + j;
-                    u[p] = gs_point(rhs[p], v1[p], v2[p], u[p - pitch], u[p - 1], u[p + pitch],
-                                    u[p + 1], c);
+                    u[p] = FM ? fm_upd_t(rhs[p] * c.rdgs, v1[p] * hh, v2[p] * hh, u[p - pitch],
+                                         u[p - 1], u[p + pitch], u[p + 1], c)
+                              : gs_point(rhs[p], v1[p], v2[p], u[p - pitch], u[p - 1],
+                                         u[p + pitch], u[p + 1], c);
                 }
             }
             __syncthreads();
@@ -537,8 +538,10 @@ __global__ __launch_bounds__(1024) void k_coarse_solve(double *u, const double *
         for (int i = 1 + ty; i <= n - 1; i += 16)
             for (int j = 1 + tx; j <= n - 1; j += 64) {
                 const long p = (long)i * pitch + j;
-                const double r = res_point(rhs[p], v1[p], v2[p], u[p], u[p - pitch], u[p - 1],
-                                           u[p + pitch], u[p + 1], c);
+                const double r = FM ? fm_res_t(rhs[p] * c.rdgs, v1[p] * hh, v2[p] * hh, u[p],
+                                               u[p - pitch], u[p - 1], u[p + pitch], u[p + 1], c)
+                                    : res_point(rhs[p], v1[p], v2[p], u[p], u[p - pitch],
+                                                u[p - 1], u[p + pitch], u[p + 1], c);
                 acc += r * r;
             }
         double s = block_sum(acc, lds);
@@ -560,6 +563,7 @@ __global__ __launch_bounds__(1024) void k_coarse_solve(double *u, const double *
 // order as k_coarse_solve, so u, the norms and the iteration count are
 // bitwise those of k_coarse_solve.
 constexpr int kCoarseLdsMaxN = 64;
+template <bool FM>
 __global__ __launch_bounds__(1024) void k_coarse_solve_lds(double *u, const double *rhs,
                                                            const double *v1, const double *v2,
                                                            int n, long pitch, Coef c, double tol,
@@ -579,9 +583,10 @@ __global__ __launch_bounds__(1024) void k_coarse_solve_lds(double *u, const doub
             const long p = (long)i * pitch + j;
             const int q = i * NP + j;
             su[q] = zero_first ? 0.0 : u[p];
-            sr[q] = rhs[p];
-            sx[q] = v1[p];
-            sy[q] = v2[p];
+            // (FM: f' = f/d and t = v*h/2, stencil.h)
+            sr[q] = FM ? rhs[p] * c.rdgs : rhs[p];
+            sx[q] = FM ? v1[p] * (c.h * 0.5) : v1[p];
+            sy[q] = FM ? v2[p] * (c.h * 0.5) : v2[p];
         }
     __syncthreads();
     int it = 0;
@@ -592,8 +597,10 @@ __global__ __launch_bounds__(1024) void k_coarse_solve_lds(double *u, const doub
                 const int jc = 1 + ((i + 1 + colour) & 1);
                 for (int j = jc + 2 * tx; j <= n - 1; j += 128) {
                     const int q = i * NP + j;
-                    su[q] = gs_point(sr[q], sx[q], sy[q], su[q - NP], su[q - 1], su[q + NP],
-                                     su[q + 1], c);
+                    su[q] = FM ? fm_upd_t(sr[q], sx[q], sy[q], su[q - NP], su[q - 1],
+                                          su[q + NP], su[q + 1], c)
+                               : gs_point(sr[q], sx[q], sy[q], su[q - NP], su[q - 1], su[q + NP],
+                                          su[q + 1], c);
                 }
             }
             __syncthreads();
@@ -602,8 +609,10 @@ __global__ __launch_bounds__(1024) void k_coarse_solve_lds(double *u, const doub
         for (int i = 1 + ty; i <= n - 1; i += 16)
             for (int j = 1 + tx; j <= n - 1; j += 64) {
                 const int q = i * NP + j;
-                const double r = res_point(sr[q], sx[q], sy[q], su[q], su[q - NP], su[q - 1],
-                                           su[q + NP], su[q + 1], c);
+                const double r = FM ? fm_res_t(sr[q], sx[q], sy[q], su[q], su[q - NP], su[q - 1],
+                                               su[q + NP], su[q + 1], c)
+                                    : res_point(sr[q], sx[q], sy[q], su[q], su[q - NP],
+                                                su[q - 1], su[q + NP], su[q + 1], c);
                 acc += r * r;
             }
         double s = block_sum(acc, lds);
@@ -717,16 +726,10 @@ long g_march_min_rows = 32;   // fewest rows per workgroup of a wave march (tuni
 void set_march_min_rows(long v) { g_march_min_rows = v; }
 long get_march_min_rows() { return g_march_min_rows; }
 
-long g_march_order = -1;   // tuning key "march_order": bit 0 bands, bit 1 XCD order
-static long march_order() {
-    if (g_march_order < 0) {
-        const char *e = getenv("MGX_MARCH_ORDER");
-        g_march_order = e ? atol(e) : 3;
-    }
-    return g_march_order;
-}
+long g_march_order = 3;   // tuning key "march_order": bit 0 bands, bit 1 XCD order
+static long march_order() { return g_march_order; }
 void set_march_order(long v) { g_march_order = v; }
-long get_march_order() { return march_order(); }
+long get_march_order() { return g_march_order; }
 
 // The work order of a launch of `upw` units per workgroup (march_order):
 // band-major with bands of upw rows on a one-region launch, and/or the
@@ -881,13 +884,22 @@ long get_coarse_lds() { return g_coarse_lds; }
 void launch_coarse_solve(double *u, const double *rhs, const double *v1, const double *v2,
                          long n, long pitch, Coef c, double tol, int maxit, bool zero_first,
                          double *stats, hipStream_t s) {
+    const int zf = zero_first ? 1 : 0;
     if (n <= kCoarseLdsMaxN && g_coarse_lds) {
-        MGX_LAUNCH(k_coarse_solve_lds, dim3(1), dim3(1024), s, u, rhs, v1, v2, (int)n, pitch, c,
-                   tol, maxit, zero_first ? 1 : 0, stats);
+        if (c.fm)
+            MGX_LAUNCH(k_coarse_solve_lds<true>, dim3(1), dim3(1024), s, u, rhs, v1, v2, (int)n,
+                       pitch, c, tol, maxit, zf, stats);
+        else
+            MGX_LAUNCH(k_coarse_solve_lds<false>, dim3(1), dim3(1024), s, u, rhs, v1, v2, (int)n,
+                       pitch, c, tol, maxit, zf, stats);
         return;
     }
-    MGX_LAUNCH(k_coarse_solve, dim3(1), dim3(1024), s, u, rhs, v1, v2, (int)n, pitch, c, tol,
-               maxit, zero_first ? 1 : 0, stats);
+    if (c.fm)
+        MGX_LAUNCH(k_coarse_solve<true>, dim3(1), dim3(1024), s, u, rhs, v1, v2, (int)n, pitch, c,
+                   tol, maxit, zf, stats);
+    else
+        MGX_LAUNCH(k_coarse_solve<false>, dim3(1), dim3(1024), s, u, rhs, v1, v2, (int)n, pitch, c,
+                   tol, maxit, zf, stats);
 }
 
 // ---------------------------------------------------------------- probes

@@ -75,14 +75,8 @@ int set_level_factors(Level &L, long row0, const std::vector<double> &a1,
 
 // Cross-cycle fusion of the finest level (k_xsmooth) on levels this large
 // (the row-march regime); tuning key "cross_cycle" turns it off.
-long g_cross_cycle = -1;
-bool cross_cycle_on() {
-    if (g_cross_cycle < 0) {
-        const char *e = getenv("MGX_CROSS_CYCLE");
-        g_cross_cycle = e ? atol(e) : 1;
-    }
-    return g_cross_cycle != 0;
-}
+long g_cross_cycle = 1;
+bool cross_cycle_on() { return g_cross_cycle != 0; }
 
 int fail(int code, const std::string &msg) {
     g_err = msg;
@@ -312,7 +306,7 @@ long g_step_fuse = 1;   // tuning key "step_fuse"
 static bool cross_ok(mgx_ctx *c) {
     const Level &L = c->lv[0];
     return cross_cycle_on() && !c->dist && c->L > 1 && L.u[2] && c->opt.smoother == 0 &&
-           c->opt.shape == 1 && (c->opt.nsmooth == 2 || c->opt.nsmooth == 3) &&
+           c->opt.shape >= 1 && (c->opt.nsmooth == 2 || c->opt.nsmooth == 3) &&
            c->opt.fuse >= c->opt.nsmooth;
 }
 
@@ -391,6 +385,10 @@ static int op_cross(mgx_ctx *c, bool store_post, bool rs = false) {
 // cycle and the pre-smoothing of the NEXT one are one k_xsmooth pass, so a
 // cycle is [pre (first cycle only) | coarse levels | cross pass]; a cycle that
 // follows one starts from the speculative state the cross pass left.
+// W-cycles (shape 2, multigrid.cpp:52): visit sh's post-smoothing of level 0
+// and visit sh+1's pre-smoothing + restriction are adjacent too, so they are
+// one cross pass as well (its u_post and norm unused): [pre | coarse | cross |
+// coarse | cross] per W-cycle instead of four level-0 passes.
 int op_vcycle(mgx_ctx *c, int l, double *norm, bool store_post) {
     if (l == 0 && norm && cross_ok(c)) {
         Level &L = c->lv[0];
@@ -399,6 +397,12 @@ int op_vcycle(mgx_ctx *c, int l, double *norm, bool store_post) {
             L.spec = -1;
         } else {
             CHK(op_smooth(c, 0, c->opt.nsmooth, false, /*restrict=*/true, false, nullptr));
+        }
+        for (int sh = 1; sh < c->opt.shape; ++sh) {
+            CHK(op_vcycle(c, 1));
+            CHK(op_cross(c, /*store_post=*/false));
+            L.cur = L.spec;   // visit sh+1 starts from the pass's u_pre
+            L.spec = -1;
         }
         CHK(op_vcycle(c, 1));
         if (c->post_only && c->step_next && mgx::xstep_supported(L.n) && L.coef.dgs > 0) {
@@ -762,6 +766,7 @@ void mgx_default_options(mgx_options *o) {
     o->max_cycle = 50;       // multigrid.cpp:94
     o->smoother = 0;
     o->fuse = 3;
+    o->fp_mode = MGX_FP_BITWISE;
 }
 
 // ---- gs.h mirror (reference layout, device pointers, null stream)
@@ -822,7 +827,7 @@ int mgxi::create_ctx(mgx_ctx **out, long n, int maxlvl, double dt, double nu,
     if (opt) o = *opt;
     if (o.fuse < 1 || o.fuse > mgx::kSmoothMaxSweeps) o.fuse = mgx::kSmoothMaxSweeps;
     if (o.nsmooth < 0 || o.shape < 1 || o.coarse_maxit < 1 || o.max_cycle < 1 ||
-        o.smoother < 0 || o.smoother > 2)
+        o.smoother < 0 || o.smoother > 2 || (o.fp_mode != MGX_FP_BITWISE && o.fp_mode != MGX_FP_FMA))
         return fail(MGX_E_ARG, "mgx_create: bad options");
     mgx_ctx *c = new mgx_ctx();
     c->N = n;
@@ -851,7 +856,7 @@ int mgxi::create_ctx(mgx_ctx **out, long n, int maxlvl, double dt, double nu,
         Level &L = c->lv[l];
         L.n = n >> l;
         L.pitch = mgx::tower_pitch(L.n);
-        L.coef = mgx::make_coef(dt, nu, h);
+        L.coef = mgx::make_coef(dt, nu, h, o.fp_mode == MGX_FP_FMA);
         h = 2 * h;
         const size_t bytes = sizeof(double) * L.pitch * (L.n + 1);
         double **bufs[5] = {&L.u[0], &L.u[1], &L.rhs, &L.v1, &L.v2};
@@ -1363,11 +1368,6 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgx::set_xfast(value);
         return MGX_OK;
     }
-    if (!strcmp(key, "xgroup")) {
-        if (value != 0 && value != 1) return fail(MGX_E_ARG, "xgroup must be 0 or 1");
-        mgx::set_xgroup(value);
-        return MGX_OK;
-    }
     if (!strcmp(key, "tile32_min_n")) {
         if (value < 0) return fail(MGX_E_ARG, "tile32_min_n must be >= 0");
         mgx::set_tile32_min_n(value);
@@ -1461,10 +1461,6 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "xfast")) {
         *value = mgx::get_xfast();
-        return MGX_OK;
-    }
-    if (!strcmp(key, "xgroup")) {
-        *value = mgx::get_xgroup();
         return MGX_OK;
     }
     if (!strcmp(key, "tile32_min_n")) {

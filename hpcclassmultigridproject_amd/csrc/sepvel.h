@@ -23,6 +23,7 @@
 #pragma once
 #include <algorithm>
 #include <atomic>
+#include <memory>
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
@@ -117,16 +118,19 @@ inline bool factor_rank1(const double *v, long rows, long w, long ld, double smi
         // every entry, bitwise (rows in parallel); columns that fail move on to
         // their next candidate, a few rounds at most
         for (int round = 0; ok && round < kC; ++round) {
-            std::vector<unsigned char> badcol(w, 0);
+            // (atomic flags: a column is counted once, on its 0 -> 1 transition)
+            std::unique_ptr<std::atomic<unsigned char>[]> badcol(
+                new std::atomic<unsigned char>[w]);
+            for (long j = 0; j < w; ++j) badcol[j].store(0, std::memory_order_relaxed);
             std::atomic<long> nbad{0};
             parallel_rows(rows, nthreads, [&](long r0, long r1) {
                 for (long i = r0; i < r1; ++i) {
                     const double *row = v + i * ld;
                     for (long j = 0; j < w; ++j)
-                        if (bits(a[i] * b[j]) != bits(row[j]) && !badcol[j]) {
-                            badcol[j] = 1;   // benign race: only ever set to 1
+                        if (bits(a[i] * b[j]) != bits(row[j]) &&
+                            !badcol[j].load(std::memory_order_relaxed) &&
+                            !badcol[j].exchange(1, std::memory_order_relaxed))
                             nbad++;
-                        }
                     if (nbad.load(std::memory_order_relaxed) > w / 4 + 8) return;
                 }
             });

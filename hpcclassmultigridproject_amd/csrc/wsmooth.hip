@@ -78,14 +78,15 @@ struct WCfg {
 // G = false: the unguarded march (interior strips, rows [TOP, n+1-BOT) of
 // WCfg: no per-stage predicates), G = true: guarded (see k_xsmooth).
 // PD: the diagonal is positive (every nu <= 0): the shorter division (div_diag).
-// MGX_WCOEF: each row's four coefficients are formed once, at its first stage
-// (as in k_xsmooth), instead of in every stage of its points.
-// (2: only the x-neighbour pair cn, cs, from t1 -- half the registers of all
-// four -- the y pair from t2 in every stage)
-#ifndef MGX_WCOEF
-#define MGX_WCOEF 2
-#endif
-template <int WPB, int K, int MODE, bool G, bool PD = false>
+// Each row's x-neighbour coefficient pair (cn, cs, from t1) is formed once, at
+// the row's first stage, the y pair (from t2) in every stage: all four per row
+// (as in k_xsmooth) needs ~110 more VGPRs -- one wave per SIMD, measured
+// slower.  (RHSN: every coefficient per stage.)
+// FM: fp_mode fma (stencil.h): f' = f/d enters the ring at the row's first
+// use, the stored pair is mn, ms, the stages contract (four fmas), residuals
+// are d*(update - u); RHSN's rhs keeps the reference expressions (gs.cpp:44,
+// stored unscaled) and is scaled after.
+template <int WPB, int K, int MODE, bool G, bool PD = false, bool FM = false>
 __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
     const double *__restrict__ uin, double *__restrict__ uout, const double *__restrict__ rhs,
     const double *__restrict__ v1, const double *__restrict__ v2, const double *__restrict__ uc,
@@ -191,9 +192,11 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
             d.x = ld2((z ? zrow : v1 + o) + cl);
             d.y = ld2((z ? zrow : v2 + o) + cl);
         };
+        // (FM: and f' = f/d; RHSN forms the rhs after this, see rhs_norm)
         auto scale_rv = [&](RowData &d) {
             d.x = make_double2(d.x.x * hh, d.x.y * hh);
             d.y = make_double2(d.y.x * hh, d.y.y * hh);
+            if (FM && !C::RHSN) d.r = make_double2(d.r.x * c.rdgs, d.r.y * c.rdgs);
         };
 
         const int s_first = a - E;
@@ -203,8 +206,7 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
 
         double2 ur[NR];
         RowData rd[NR];
-        constexpr bool WC = MGX_WCOEF == 1 && !C::RHSN;
-        constexpr bool WH = MGX_WCOEF == 2 && !C::RHSN;   // half: cn, cs stored
+        constexpr bool WH = !C::RHSN;   // cn, cs stored per row
         CoefRow cf[NR];
 #pragma unroll
         for (int q = 0; q < NR; ++q) {
@@ -213,25 +215,25 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
             const double2 z = make_double2(0.0, 0.0);
             cf[q] = CoefRow{z, z, z, z};
         }
-        // gs.cpp:126-129 coefficients of a row's two points from t1, t2
-        auto to_coef = [&](const RowData &d, CoefRow &k) {
-            k.cn = make_double2(c.rr * (c.nu - d.x.x), c.rr * (c.nu - d.x.y));
-            k.cw = make_double2(c.rr * (c.nu - d.y.x), c.rr * (c.nu - d.y.y));
-            k.cs = make_double2(c.rr * (d.x.x + c.nu), c.rr * (d.x.y + c.nu));
-            k.ce = make_double2(c.rr * (d.y.x + c.nu), c.rr * (d.y.y + c.nu));
-        };
-        // residual (gs.cpp:75 term order) of the row in slot iR, column c0 / c0+1
+        // residual (gs.cpp:75 term order) of the row in slot iR, column c0 / c0+1,
+        // from its stored cn, cs (FM: mn, ms)
         auto res_cx = [&](const int iR, const int iN, const int iS, const double uW) {
             const CoefRow &k = cf[iR];
-            const double cw = MGX_WCOEF == 2 ? c.rr * (c.nu - rd[iR].y.x) : k.cw.x;
-            const double ce = MGX_WCOEF == 2 ? c.rr * (rd[iR].y.x + c.nu) : k.ce.x;
+            const double t2 = rd[iR].y.x;
+            if (FM)
+                return fm_res(rd[iR].r.x, ur[iR].x, k.cn.x, ur[iN].x, fm_mp(t2, c), uW, k.cs.x,
+                              ur[iS].x, fm_mm(t2, c), ur[iR].y, c);
+            const double cw = c.rr * (c.nu - t2), ce = c.rr * (t2 + c.nu);
             return rd[iR].r.x - (c.dgs * ur[iR].x + k.cn.x * ur[iN].x + cw * uW +
                                  k.cs.x * ur[iS].x + ce * ur[iR].y);
         };
         auto res_cy = [&](const int iR, const int iN, const int iS, const double uE) {
             const CoefRow &k = cf[iR];
-            const double cw = MGX_WCOEF == 2 ? c.rr * (c.nu - rd[iR].y.y) : k.cw.y;
-            const double ce = MGX_WCOEF == 2 ? c.rr * (rd[iR].y.y + c.nu) : k.ce.y;
+            const double t2 = rd[iR].y.y;
+            if (FM)
+                return fm_res(rd[iR].r.y, ur[iR].y, k.cn.y, ur[iN].y, fm_mp(t2, c), ur[iR].x,
+                              k.cs.y, ur[iS].y, fm_mm(t2, c), uE, c);
+            const double cw = c.rr * (c.nu - t2), ce = c.rr * (t2 + c.nu);
             return rd[iR].r.y - (c.dgs * ur[iR].y + k.cn.y * ur[iN].y + cw * ur[iR].x +
                                  k.cs.y * ur[iS].y + ce * uE);
         };
@@ -262,11 +264,11 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                                           ur[iR].y, cg);
             const double f1 = rhs_point_t(d.x.y, d.y.y, ur[iR].y, ur[iN].y, ur[iR].x, ur[iS].y,
                                           uE, cg);
-            d.r = make_double2(f0, f1);
+            d.r = FM ? make_double2(f0 * c.rdgs, f1 * c.rdgs) : make_double2(f0, f1);
             if (rowin(r) && r >= 1 && r <= n - 1 && keep) {
                 double *row = rhs_out + rowoff(r, ip);
                 if (in0 && in1) {
-                    st2(row + c0, d.r);
+                    st2(row + c0, make_double2(f0, f1));
                 } else {
                     if (in0) row[c0] = f0;
                     if (in1) row[c0 + 1] = f1;
@@ -296,12 +298,16 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                 load_u(s + 5, up[(p + 1) & 1], (p + 1) & 1);
                 // t of the row first used in this step: s+2 (RHSN), else s+1
                 scale_rv(rd[(p + (C::RHSN ? 2 : 1)) % NR]);
-                if (WC) to_coef(rd[(p + 1) % NR], cf[(p + 1) % NR]);
                 if (WH) {   // cn, cs of row s+1 from t1 (gs.cpp:128-129's cc, dd)
                     const RowData &d1 = rd[(p + 1) % NR];
                     CoefRow &k1 = cf[(p + 1) % NR];
-                    k1.cn = make_double2(c.rr * (c.nu - d1.x.x), c.rr * (c.nu - d1.x.y));
-                    k1.cs = make_double2(c.rr * (d1.x.x + c.nu), c.rr * (d1.x.y + c.nu));
+                    if (FM) {
+                        k1.cn = make_double2(fm_mp(d1.x.x, c), fm_mp(d1.x.y, c));
+                        k1.cs = make_double2(fm_mm(d1.x.x, c), fm_mm(d1.x.y, c));
+                    } else {
+                        k1.cn = make_double2(c.rr * (c.nu - d1.x.x), c.rr * (c.nu - d1.x.y));
+                        k1.cs = make_double2(c.rr * (d1.x.x + c.nu), c.rr * (d1.x.y + c.nu));
+                    }
                 }
                 // rows s+1..s+3 are still original u: rhs of row s+2
                 if (C::RHSN) rhs_norm(s + 2, (p + 2) % NR, (p + 1) % NR, (p + 3) % NR);
@@ -324,15 +330,17 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                     if (cs == 0) {
                         const double uW = dpp_shr1(ur[iR].y);   // column c0-1
                         if (!G || (inr && in0)) {
-                            if (WH)
+                            if (FM && WH)
+                                ur[iR].x = fm_upd(d.r.x, k.cn.x, ur[iN].x, fm_mp(d.y.x, cg), uW,
+                                                  k.cs.x, ur[iS].x, fm_mm(d.y.x, cg), ur[iR].y);
+                            else if (FM)
+                                ur[iR].x = fm_upd_t(d.r.x, d.x.x, d.y.x, ur[iN].x, uW, ur[iS].x,
+                                                    ur[iR].y, cg);
+                            else if (WH)
                                 ur[iR].x = div_diag<PD>(d.r.x - k.cn.x * ur[iN].x -
                                                             cg.rr * (cg.nu - d.y.x) * uW -
                                                             k.cs.x * ur[iS].x -
                                                             cg.rr * (d.y.x + cg.nu) * ur[iR].y,
-                                                        c);
-                            else if (WC)
-                                ur[iR].x = div_diag<PD>(d.r.x - k.cn.x * ur[iN].x - k.cw.x * uW -
-                                                            k.cs.x * ur[iS].x - k.ce.x * ur[iR].y,
                                                         c);
                             else
                                 ur[iR].x = gs_point_t<PD>(d.r.x, d.x.x, d.y.x, ur[iN].x, uW,
@@ -341,16 +349,18 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                     } else {
                         const double uE = dpp_shl1(ur[iR].x);   // column c0+2
                         if (!G || (inr && in1)) {
-                            if (WH)
+                            if (FM && WH)
+                                ur[iR].y = fm_upd(d.r.y, k.cn.y, ur[iN].y, fm_mp(d.y.y, cg),
+                                                  ur[iR].x, k.cs.y, ur[iS].y, fm_mm(d.y.y, cg),
+                                                  uE);
+                            else if (FM)
+                                ur[iR].y = fm_upd_t(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x,
+                                                    ur[iS].y, uE, cg);
+                            else if (WH)
                                 ur[iR].y = div_diag<PD>(d.r.y - k.cn.y * ur[iN].y -
                                                             cg.rr * (cg.nu - d.y.y) * ur[iR].x -
                                                             k.cs.y * ur[iS].y -
                                                             cg.rr * (d.y.y + cg.nu) * uE,
-                                                        c);
-                            else if (WC)
-                                ur[iR].y = div_diag<PD>(d.r.y - k.cn.y * ur[iN].y -
-                                                            k.cw.y * ur[iR].x - k.cs.y * ur[iS].y -
-                                                            k.ce.y * uE,
                                                         c);
                             else
                                 ur[iR].y = gs_point_t<PD>(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x,
@@ -374,7 +384,10 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                     const double uW = dpp_shr1(ur[iR].y);
                     // (the same expressions from the row's coefficients, bitwise)
                     auto rx = [&]() {
-                        if (WC || WH) return res_cx(iR, iN, iS, uW);
+                        if (WH) return res_cx(iR, iN, iS, uW);
+                        if (FM)
+                            return fm_res_t(d.r.x, d.x.x, d.y.x, ur[iR].x, ur[iN].x, uW, ur[iS].x,
+                                            ur[iR].y, c);
                         return res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x, ur[iN].x, uW, ur[iS].x,
                                            ur[iR].y, c);
                     };
@@ -387,7 +400,10 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                     } else {
                         const double uE = dpp_shl1(ur[iR].x);
                         auto ry = [&]() {
-                            if (WC || WH) return res_cy(iR, iN, iS, uE);
+                            if (WH) return res_cy(iR, iN, iS, uE);
+                            if (FM)
+                                return fm_res_t(d.r.y, d.x.y, d.y.y, ur[iR].y, ur[iN].y, ur[iR].x,
+                                                ur[iS].y, uE, c);
                             return res_point_t(d.r.y, d.x.y, d.y.y, ur[iR].y, ur[iN].y, ur[iR].x,
                                                ur[iS].y, uE, c);
                         };
@@ -449,7 +465,9 @@ struct TileCfg {
     static constexpr int PPT = (PAIRS + THREADS - 1) / THREADS;   // pairs per thread
 };
 
-template <int K, int MODE, int TRV>
+// FM: fp_mode fma (stencil.h): f' = f/d and t = v*h/2 kept per pair, the
+// contracted update and residual from them.
+template <int K, int MODE, int TRV, bool FM>
 __global__ __launch_bounds__(MGX_TILE_THREADS) void k_smooth_tile(
     const double *__restrict__ uin, double *__restrict__ uout, const double *__restrict__ rhs,
     const double *__restrict__ v1, const double *__restrict__ v2, const double *__restrict__ uc,
@@ -510,12 +528,13 @@ __global__ __launch_bounds__(MGX_TILE_THREADS) void k_smooth_tile(
                 v.y = v.y + pr.y;
             }
             const double2 rr = ld2(rhs + o), xx = ld2(v1 + o), yy = ld2(v2 + o);
-            f0[m] = rr.x;
-            f1[m] = rr.y;
-            x0[m] = xx.x;
-            x1[m] = xx.y;
-            y0[m] = yy.x;
-            y1[m] = yy.y;
+            f0[m] = FM ? rr.x * c.rdgs : rr.x;
+            f1[m] = FM ? rr.y * c.rdgs : rr.y;
+            const double hh = FM ? c.h * 0.5 : 1.0;   // (an exact no-op scaling otherwise)
+            x0[m] = FM ? xx.x * hh : xx.x;
+            x1[m] = FM ? xx.y * hh : xx.y;
+            y0[m] = FM ? yy.x * hh : yy.x;
+            y1[m] = FM ? yy.y * hh : yy.y;
         }
         tu[(r & 1) * PL + q] = v.x;   // q = r*HW + k
         tu[((r & 1) ^ 1) * PL + q] = v.y;
@@ -557,13 +576,21 @@ __global__ __launch_bounds__(MGX_TILE_THREADS) void k_smooth_tile(
             const double *oth = tu + ((h & 1) ^ 1) * PL;   // its neighbours
             const double fr = cs ? f1[m] : f0[m], fx = cs ? x1[m] : x0[m],
                          fy = cs ? y1[m] : y0[m];
-            own[b] = gs_point_fast(fr, fx, fy, oth[b - HW], oth[b - 1 + cs], oth[b + HW],
-                                   oth[b + cs], c);
+            own[b] = FM ? fm_upd_t(fr, fx, fy, oth[b - HW], oth[b - 1 + cs], oth[b + HW],
+                                   oth[b + cs], c)
+                        : gs_point_fast(fr, fx, fy, oth[b - HW], oth[b - 1 + cs], oth[b + HW],
+                                        oth[b + cs], c);
         }
         __syncthreads();
     }
 
     double acc = 0.0;
+    // gs.cpp:75 (FM: d*(update - u))
+    auto tres = [&](double f, double x, double y, double u, double uN, double uW, double uS,
+                    double uE, const Coef &cc) {
+        return FM ? fm_res_t(f, x, y, u, uN, uW, uS, uE, cc)
+                  : res_point(f, x, y, u, uN, uW, uS, uE, cc);
+    };
 #pragma unroll
     for (int m = 0; m < PPT; ++m) {
         const int q = t + m * T::THREADS;
@@ -581,16 +608,16 @@ __global__ __launch_bounds__(MGX_TILE_THREADS) void k_smooth_tile(
             if (C::REST) {
                 if (!(gi & 1) && in0 && gi <= n - 2 && gj <= n - 2)
                     rhsc[(gi >> 1) * pitchc + (gj >> 1)] =
-                        res_point(f0[m], x0[m], y0[m], p0[b], p1[b - HW], p1[b - 1], p1[b + HW],
+                        tres(f0[m], x0[m], y0[m], p0[b], p1[b - HW], p1[b - 1], p1[b + HW],
                                   p1[b], c);
             } else {
                 if (in0) {
-                    const double res = res_point(f0[m], x0[m], y0[m], p0[b], p1[b - HW],
+                    const double res = tres(f0[m], x0[m], y0[m], p0[b], p1[b - HW],
                                                  p1[b - 1], p1[b + HW], p1[b], c);
                     acc += res * res;
                 }
                 if (in1) {
-                    const double res = res_point(f1[m], x1[m], y1[m], p1[b], p0[b - HW],
+                    const double res = tres(f1[m], x1[m], y1[m], p1[b], p0[b - HW],
                                                  p0[b], p0[b + HW], p0[b + 1], c);
                     acc += res * res;
                 }
@@ -606,7 +633,7 @@ __global__ __launch_bounds__(MGX_TILE_THREADS) void k_smooth_tile(
 
 }  // namespace
 
-template <int WPB, int K, int MODE, bool G, bool PD>
+template <int WPB, int K, int MODE, bool G, bool PD, bool FM>
 static int wsmooth_launch_pd(const SmoothArgs &A, const MarchRegions &reg, double *partials,
                              long max_wgs, hipStream_t s) {
     const long total = reg.pre[reg.count];
@@ -616,7 +643,7 @@ static int wsmooth_launch_pd(const SmoothArgs &A, const MarchRegions &reg, doubl
         int dev = 0, cus = 0, per = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_wsmooth<WPB, K, MODE, G, PD>,
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_wsmooth<WPB, K, MODE, G, PD, FM>,
                                                            64 * WPB, 0);
         slots = std::max(1, cus) * std::max(1, per);
     }
@@ -628,7 +655,7 @@ static int wsmooth_launch_pd(const SmoothArgs &A, const MarchRegions &reg, doubl
     // strips); the same per rank on 8 row blocks
     const unsigned grid = plan_march(reg, WPB, slots, get_march_min_rows(), max_wgs,
                                      WCfg<K, MODE>::E + WCfg<K, MODE>::NR / 2, upw, r);
-    MGX_LAUNCH((k_wsmooth<WPB, K, MODE, G, PD>), dim3(grid), dim3(64 * WPB), s, A.uin, A.uout,
+    MGX_LAUNCH((k_wsmooth<WPB, K, MODE, G, PD, FM>), dim3(grid), dim3(64 * WPB), s, A.uin, A.uout,
                A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch, r, upw,
                A.c, A.lo, A.hi, A.rhs_out, A.zrow ? A.zrow : A.v1, A.zrow ? A.vz : 0x7fffffff);
     return (int)grid * WPB;   // NORM partials written
@@ -637,8 +664,11 @@ static int wsmooth_launch_pd(const SmoothArgs &A, const MarchRegions &reg, doubl
 template <int WPB, int K, int MODE, bool G>
 static int wsmooth_launch(const SmoothArgs &A, const MarchRegions &reg, double *partials,
                           long max_wgs, hipStream_t s) {
-    if (A.c.dgs > 0) return wsmooth_launch_pd<WPB, K, MODE, G, true>(A, reg, partials, max_wgs, s);
-    return wsmooth_launch_pd<WPB, K, MODE, G, false>(A, reg, partials, max_wgs, s);
+    // (fp_mode fma: no division)
+    if (A.c.fm) return wsmooth_launch_pd<WPB, K, MODE, G, false, true>(A, reg, partials, max_wgs, s);
+    if (A.c.dgs > 0)
+        return wsmooth_launch_pd<WPB, K, MODE, G, true, false>(A, reg, partials, max_wgs, s);
+    return wsmooth_launch_pd<WPB, K, MODE, G, false, false>(A, reg, partials, max_wgs, s);
 }
 
 // One guarded launch over the whole level.  (The interior / edge split that
@@ -653,45 +683,18 @@ static int smooth_winst(const SmoothArgs &A, hipStream_t s) {
     return wsmooth_launch<WPB, K, MODE, true>(A, edge, A.partials, kNormBlocks / WPB, s);
 }
 
-long g_tile_max_n = -1;   // levels with n <= this use k_smooth_tile
-
+// levels with n <= tile_max_n use k_smooth_tile (tuning key "tile_max_n"):
+// 1024 = level 3 (n = 2048) as a wave march, 0.115 -> 0.105-0.110 ms per
+// cycle at N=16384 (tools/ab_levels.py); levels 4-5 measure the same either way
+long g_tile_max_n = 1024;
 void set_tile_max_n(long v) { g_tile_max_n = v; }
-long get_tile_max_n();
-
-static long tile_max_n() {
-    if (g_tile_max_n < 0) {
-        const char *e = getenv("MGX_TILE_MAX_N");
-        // 1024: level 3 (n = 2048) as a wave march, 0.115 -> 0.105-0.110 ms
-        // per cycle at N=16384 (tools/ab_levels.py); levels 4-5 measure the
-        // same either way
-        g_tile_max_n = e ? atol(e) : 1024;
-    }
-    return g_tile_max_n;
-}
-
-long get_tile_max_n() { return tile_max_n(); }
-
-long g_tile32_min_n = -1;   // 32-row tiles on levels n >= this (tuning key "tile32_min_n")
-long g_tile_xcd = -1;       // XCD-contiguous tile order (tuning key "tile_xcd")
-
-static long tile32_min_n() {
-    if (g_tile32_min_n < 0) {
-        const char *e = getenv("MGX_TILE32_MIN_N");
-        g_tile32_min_n = e ? atol(e) : 2048;
-    }
-    return g_tile32_min_n;
-}
+long get_tile_max_n() { return g_tile_max_n; }
+long g_tile32_min_n = 2048;   // 32-row tiles on levels n >= this (tuning key "tile32_min_n")
 void set_tile32_min_n(long v) { g_tile32_min_n = v; }
-long get_tile32_min_n() { return tile32_min_n(); }
-static long tile_xcd() {
-    if (g_tile_xcd < 0) {
-        const char *e = getenv("MGX_TILE_XCD");
-        g_tile_xcd = e ? atol(e) : 1;
-    }
-    return g_tile_xcd;
-}
+long get_tile32_min_n() { return g_tile32_min_n; }
+long g_tile_xcd = 1;          // XCD-contiguous tile order (tuning key "tile_xcd")
 void set_tile_xcd(long v) { g_tile_xcd = v; }
-long get_tile_xcd() { return tile_xcd(); }
+long get_tile_xcd() { return g_tile_xcd; }
 
 template <int K, int MODE, int TRV>
 static int smooth_tile_rows(const SmoothArgs &A, hipStream_t s) {
@@ -701,9 +704,14 @@ static int smooth_tile_rows(const SmoothArgs &A, hipStream_t s) {
     const int tiles_y = (int)((A.rb - A.ra + T::TR - 1) / T::TR);
     const long grid = (long)tiles_x * tiles_y;
     if ((MODE & 8) && grid > kNormBlocks) return -1;
-    MGX_LAUNCH((k_smooth_tile<K, MODE, TRV>), dim3((unsigned)grid), dim3(T::THREADS), s, A.uin,
-               A.uout, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, A.partials, (int)n, A.pitch,
-               tiles_x, A.c, A.ra, A.rb, A.lo, A.hi, tile_xcd() ? 1 : 0);
+    if (A.c.fm)
+        MGX_LAUNCH((k_smooth_tile<K, MODE, TRV, true>), dim3((unsigned)grid), dim3(T::THREADS), s,
+                   A.uin, A.uout, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, A.partials, (int)n,
+                   A.pitch, tiles_x, A.c, A.ra, A.rb, A.lo, A.hi, g_tile_xcd ? 1 : 0);
+    else
+        MGX_LAUNCH((k_smooth_tile<K, MODE, TRV, false>), dim3((unsigned)grid), dim3(T::THREADS), s,
+                   A.uin, A.uout, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, A.partials, (int)n,
+                   A.pitch, tiles_x, A.c, A.ra, A.rb, A.lo, A.hi, g_tile_xcd ? 1 : 0);
     return (int)grid;
 }
 
@@ -712,7 +720,7 @@ static int smooth_tile_rows(const SmoothArgs &A, hipStream_t s) {
 template <int K, int MODE>
 static int smooth_tile_inst(const SmoothArgs &A, hipStream_t s) {
     if constexpr (K == 3)
-        if (A.n >= tile32_min_n()) return smooth_tile_rows<K, MODE, 32>(A, s);
+        if (A.n >= g_tile32_min_n) return smooth_tile_rows<K, MODE, 32>(A, s);
     return smooth_tile_rows<K, MODE, 16>(A, s);
 }
 
@@ -729,7 +737,7 @@ static int smooth_block(const SmoothArgs &A, hipStream_t s) {
     // the row march needs >= ~32 rows per wave to amortise its priming rows;
     // a row block too small to give every resident wave that much (a
     // partitioned level on many GPUs) runs as LDS tiles instead
-    bool tile = A.n <= tile_max_n() && !(MODE & 16);   // RHSN: march only
+    bool tile = A.n <= g_tile_max_n && !(MODE & 16);   // RHSN: march only
     if (!tile && !(MODE & 16)) {
         constexpr int W4 = WCfg<K, MODE>::W * 4;
         static int slots = 0;

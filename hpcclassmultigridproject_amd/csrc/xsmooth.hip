@@ -93,36 +93,13 @@ struct XCfg {
 // exact (sepvel.h checks the range) -- from the lane's column factors, held
 // in registers for the whole march.
 //
-// XG = true (group exchange, unguarded only): the WPB pairs of a workgroup
-// march WPB ADJACENT 128-column strips that overlap by nothing, and the
-// workgroup as a whole is one 64*WPB-lane strip with the H-pair halo only on
-// its two outer sides: group g owns WGc = 128*WPB - 4H columns (484 instead of
-// 4 x 100).  The columns a wave's edge lanes need from the neighbouring wave
-// of the same role (lane 0 the west wave's column c0-1, lane 63 the east
-// wave's column c0+2) come through LDS: all inputs of a march step's stages
-// and residuals from a neighbouring column are results of the PREVIOUS step
-// (a stage on row r updates one colour; the other colour of row r was last
-// updated by the stage before, one step earlier, or is the row's initial
-// value), so each wave posts, at the end of a step, lane 0's .x and lane 63's
-// .y of every row it changed (and of the row that entered its ring), and a
-// barrier per step (instead of per two steps) orders post and use.  The
-// edge lane takes the posted value through the DPP shift's "keep old" form
-// (bound_ctrl off): no extra VALU instruction.  The halo work of the pass
-// drops from 28 of 128 columns to 28 of 512.
-// rhs row prefetch distance of the XG kernel (its exchange values take the
-// registers of one prefetched row)
-#ifndef MGX_XGRV
-#define MGX_XGRV 3
-#endif
-#ifndef MGX_XG_DBG
-#define MGX_XG_DBG 0
-#endif
-struct XGeo {
-    int x0, xl, xend, glast;   // XG: owned origin of group 0, origin of the last group, end
-    int ec0, ec1, er0, er1;    // guarded kernel: [ec0, ec1) x [er0, er1) owned by the XG launch
-};
-
-template <int WPB, int K, bool G, bool RS = false, bool SV = false, bool XG = false>
+// FM = true (fp_mode fma, stencil.h): each row's rhs enters the ring as f' =
+// f/d at its first use (A: the row's first stage, before the hand-off, so B
+// receives it scaled), the per-row coefficients are the m = -c/d of the
+// contracted update (one fma each), every update is four fmas and every
+// residual d*(update - u).  B's time-step rhs (RS) keeps the reference
+// expressions (gs.cpp:44, stored unscaled) and is scaled after.
+template <int WPB, int K, bool G, bool RS = false, bool SV = false, bool FM = false>
 __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     const double *__restrict__ uin, double *__restrict__ upost, double *__restrict__ upre,
     const double *__restrict__ rhs, const double *__restrict__ v1, const double *__restrict__ v2,
@@ -131,18 +108,16 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     int lo, int hi, int store_post, double *__restrict__ rhs_next,
     double *__restrict__ partials2, const double *__restrict__ sa1,
     const double *__restrict__ sb1, const double *__restrict__ sa2,
-    const double *__restrict__ sb2, XGeo xg) {
+    const double *__restrict__ sb2) {
     using X = XCfg<K>;
     constexpr int S = X::S, H = X::H, NR = X::NR, W = X::W, D = X::D, NU = X::NU,
                   NRD = X::NRD, EA = X::EA, EB = X::EB;
-    static_assert(!XG || !G, "the group exchange is the unguarded kernel's");
-    constexpr int WGc = 128 * WPB - 4 * H;
     // A's prefetch distances in steps: rhs/v rows XRV ahead of their first
     // stage, u rows (+ coarse parents) XU ahead of entering the ring.  The
     // pass is bound by loads in flight, not by VALU: rhs/v 2 -> 3 -> 4 steps
     // took level 0 -4 % and -3 % at the same VGPR count (B's path sets it);
     // u 3-4 steps or rhs/v 5 measured no better (N=16384, tools/ab_libs.sh).
-    constexpr int XRV = XG ? MGX_XGRV : MGX_XRV;
+    constexpr int XRV = MGX_XRV;
     constexpr int XU = MGX_XU;
     // A forms each row's coefficients once (MGX_XACOEF; B always does).  Not
     // in the guarded edge kernel: there it takes the kernel past 256 VGPRs
@@ -155,13 +130,6 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     __shared__ double2 uring[WPB][NU][64];
     // rhs / t1 / t2 planes: each hand-off access is 16 B per lane, unit stride
     __shared__ double2 rdring[WPB][NRD][3][64];
-    // XG: per role and wave, lane 0's .x (xchx) and lane 63's .y (xchy) of
-    // each ring row, slot = row mod NR (the register rings' index)
-    // (entries 0 and WPB+1 of each role: the outer waves' outer neighbours,
-    // never written -- read only by halo lanes -- so that a wave's own, west
-    // and east entries sit at fixed offsets from one address)
-    // [role][wave + 1][0: lane 0's .x, 1: lane 63's .y][slot]
-    __shared__ double xch[XG ? 2 : 1][XG ? WPB + 2 : 1][2][XG ? NR : 1];
 
     const int l = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
@@ -184,51 +152,9 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
         constexpr bool GM = G, GS = G, GN = G;   // make_u / stage / residual guards
         const int c0 = cb + 2 * l;
         const bool act = c0 >= 0 && c0 <= n;
-        // the guarded kernel beside an XG launch: rows [er0, er1) of columns
-        // [ec0, ec1) are that launch's (one owner per output)
-        const bool exc = G && c0 >= xg.ec0 && c0 < xg.ec1;
         const bool keep = act && c0 >= k0 && c0 < k1;
         // (rows [a, b) as one unsigned compare: b >= a)
-        auto own = [&](const int r) {
-            return (unsigned)(r - a) < (unsigned)(b - a) && keep &&
-                   !(exc && r >= xg.er0 && r < xg.er1);
-        };
-        // XG: the neighbouring waves of this role (the outer waves' outer
-        // edge lanes are halo: any value will do, their own slot)
-        const int rl = isA ? 0 : 1;
-        const int pw = pr, pme = pr + 1, pe = pr + 2;
-        // west neighbour of column c0 / east neighbour of column c0+1 of the
-        // row in ring slot i: DPP shifts, the edge lane's from the neighbouring
-        // wave's post (XG) or 0 (a halo lane)
-        auto nbw = [&](const double y, const int i) {
-            if (!XG || MGX_XG_DBG == 1) return dpp_shr1(y);
-            return dpp_shr1_or(y, xch[rl][pw][1][i]);
-        };
-        auto nbe = [&](const double x, const int i) {
-            if (!XG || MGX_XG_DBG == 1) return dpp_shl1(x);
-            return dpp_shl1_or(x, xch[rl][pe][0][i]);
-        };
-        // XG: at the end of a step at ring phase q, post lane 0's .x / lane
-        // 63's .y of the rows its stages changed (stage h, row slot q+1-h,
-        // updates .x iff its colour cs = 0) and of the row that entered the
-        // ring (slot q+3)
-        auto post_edges = [&](const double2 *ur, const int q) {
-            if (!XG || MGX_XG_DBG == 2) return;
-            if (l == 0) {
-#pragma unroll
-                for (int h = 0; h < S; ++h)
-                    if ((((q + 1 - h) & 1) ^ (h & 1)) == 0)
-                        xch[rl][pme][0][(q + 1 - h + 2 * NR) % NR] = ur[(q + 1 - h + 2 * NR) % NR].x;
-                xch[rl][pme][0][(q + 3) % NR] = ur[(q + 3) % NR].x;
-            }
-            if (l == 63) {
-#pragma unroll
-                for (int h = 0; h < S; ++h)
-                    if ((((q + 1 - h) & 1) ^ (h & 1)) == 1)
-                        xch[rl][pme][1][(q + 1 - h + 2 * NR) % NR] = ur[(q + 1 - h + 2 * NR) % NR].y;
-                xch[rl][pme][1][(q + 3) % NR] = ur[(q + 3) % NR].y;
-            }
-        };
+        auto own = [&](const int r) { return (unsigned)(r - a) < (unsigned)(b - a) && keep; };
         const bool in0 = act && c0 >= 1 && c0 <= n - 1;
         const bool in1 = act && c0 + 1 <= n - 1;
         const int cl = min(max(c0, 0), (int)pitch - 2);
@@ -243,10 +169,15 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             double q00, q01, q10, q11;
         };
         RowData rd[NR];   // rhs / t1 / t2 rows (ring by row)
+        double2 ur[NR];   // u rows (ring by row)
         // u rows + coarse parents in flight, a ring by row like rd
         UPre up[NR];
 #pragma unroll
-        for (int i = 0; i < NR; ++i) up[i] = UPre{make_double2(0.0, 0.0), 0.0, 0.0, 0.0, 0.0};
+        for (int i = 0; i < NR; ++i) {
+            up[i] = UPre{make_double2(0.0, 0.0), 0.0, 0.0, 0.0, 0.0};
+            ur[i] = make_double2(0.0, 0.0);
+            rd[i].r = rd[i].x = rd[i].y = make_double2(0.0, 0.0);
+        }
         // A: u row R + its coarse parents (odd = R's parity, compile-time:
         // an even row needs only the coarse row below it)
         auto load_u = [&](int R, UPre &u, const bool odd) {
@@ -303,14 +234,18 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                 d.y = make_double2(y.x * hh, y.y * hh);
             }
         };
-        // SV: t of the row in slot q, at its first stage
-        auto make_t = [&](const int q) {
-            if (!SV) return;
-            rd[q].x = make_double2(ar1[q] * bh1.x, ar1[q] * bh1.y);
-            rd[q].y = make_double2(ar2[q] * bh2.x, ar2[q] * bh2.y);
+        // A, the row in slot q at its first stage: t from the factors (SV),
+        // and f' = f/d (FM)
+        auto first_use = [&](const int q) {
+            if (SV) {
+                rd[q].x = make_double2(ar1[q] * bh1.x, ar1[q] * bh1.y);
+                rd[q].y = make_double2(ar2[q] * bh2.x, ar2[q] * bh2.y);
+            }
+            if (FM) rd[q].r = make_double2(rd[q].r.x * c.rdgs, rd[q].r.y * c.rdgs);
         };
-        // one red-black stage h of the march step at row phase p on row r
-        auto stage = [&](double2 *ur, RowData *rd, const int p, const int h, const int r) {
+        // one red-black stage h of the march step at row phase p on row r,
+        // the coefficients from t (A's stages in the guarded kernel)
+        auto stage = [&](const int p, const int h, const int r) {
             const int iR = (p + 1 - h + 2 * NR) % NR;
             const int iN = (p - h + 2 * NR) % NR;
             const int iS = (p + 2 - h + 2 * NR) % NR;
@@ -325,42 +260,54 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             if (!GS) asm volatile("" : "+s"(cg.nu));
             // (the unguarded kernel only runs with d > 0: xsmooth_inst)
             if (cs == 0) {
-                const double uW = nbw(ur[iR].y, iR);
+                const double uW = dpp_shr1(ur[iR].y);
                 if (!GS || (inr && in0))
-                    ur[iR].x = gs_point_t<!GS>(d.r.x, d.x.x, d.y.x, ur[iN].x, uW, ur[iS].x,
-                                               ur[iR].y, cg);
+                    ur[iR].x = FM ? fm_upd_t(d.r.x, d.x.x, d.y.x, ur[iN].x, uW, ur[iS].x,
+                                             ur[iR].y, c)
+                                  : gs_point_t<!GS>(d.r.x, d.x.x, d.y.x, ur[iN].x, uW, ur[iS].x,
+                                                    ur[iR].y, cg);
             } else {
-                const double uE = nbe(ur[iR].x, iR);
+                const double uE = dpp_shl1(ur[iR].x);
                 if (!GS || (inr && in1))
-                    ur[iR].y = gs_point_t<!GS>(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x,
-                                               ur[iS].y, uE, cg);
+                    ur[iR].y = FM ? fm_upd_t(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x, ur[iS].y,
+                                             uE, c)
+                                  : gs_point_t<!GS>(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x,
+                                                    ur[iS].y, uE, cg);
             }
+        };
+        // residual of the row in slot iR at column c0 / c0+1 from its t
+        // (gs.cpp:75 term order; FM: d*(update - u))
+        auto res_tx = [&](const int iR, const int iN, const int iS, const double uW) {
+            const RowData &d = rd[iR];
+            return FM ? fm_res_t(d.r.x, d.x.x, d.y.x, ur[iR].x, ur[iN].x, uW, ur[iS].x, ur[iR].y,
+                                 c)
+                      : res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x, ur[iN].x, uW, ur[iS].x,
+                                    ur[iR].y, c);
+        };
+        auto res_ty = [&](const int iR, const int iN, const int iS, const double uE) {
+            const RowData &d = rd[iR];
+            return FM ? fm_res_t(d.r.y, d.x.y, d.y.y, ur[iR].y, ur[iN].y, ur[iR].x, ur[iS].y, uE,
+                                 c)
+                      : res_point_t(d.r.y, d.x.y, d.y.y, ur[iR].y, ur[iN].y, ur[iR].x, ur[iS].y,
+                                    uE, c);
         };
 
         // A's first step (aligned to NR so ring indices and parities are
         // static); B runs D steps behind; the last iteration is B's last step
         // (rounded up to whole pairs: an extra step stores nothing)
-        // (XG: 2 rows earlier -- the prologue's first rows s0+1, s0+2 enter
-        // the ring unposted, so the neighbouring waves' warm-up garbage
-        // reaches 2 rows further down than a lone strip's)
-        int s0 = a - EB - EA - (RS ? 1 : 0) - (XG ? 2 : 0);
+        int s0 = a - EB - EA - (RS ? 1 : 0);
         s0 = s0 >= 0 ? (s0 / NR) * NR : -(((-s0) + NR - 1) / NR) * NR;
         s0 = __builtin_amdgcn_readfirstlane(s0);
         const int iters = ((b + EB - 3) + D - s0 + 1 + 1) & ~1;
         const bool post = store_post != 0;
 
-        double2 ur[NR];
-#pragma unroll
-        for (int q = 0; q < NR; ++q) {
-            ur[q] = make_double2(0.0, 0.0);
-            rd[q].r = rd[q].x = rd[q].y = make_double2(0.0, 0.0);
-        }
         // B turns each rhs/v row's t1, t2 into the four coefficients of its
         // two points once (gs.cpp:126-129, the expressions of gs_point_t),
         // just before the row's first stage, instead of in each of the
         // point's three stages and its restriction residual: -12 % VALU per
         // pass, -3 % time (the same in A as well: -23 % VALU, no further
         // time, 254 instead of 224 VGPRs -- the pass is not issue bound)
+        // (FM: the m = -c/d of the contracted update)
         CoefRow cf[NR];
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
@@ -368,6 +315,13 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             cf[i] = CoefRow{z, z, z, z};
         }
         auto to_coef = [&](const RowData &d, CoefRow &k) {
+            if (FM) {
+                k.cn = make_double2(fm_mp(d.x.x, c), fm_mp(d.x.y, c));
+                k.cw = make_double2(fm_mp(d.y.x, c), fm_mp(d.y.y, c));
+                k.cs = make_double2(fm_mm(d.x.x, c), fm_mm(d.x.y, c));
+                k.ce = make_double2(fm_mm(d.y.x, c), fm_mm(d.y.y, c));
+                return;
+            }
             k.cn = make_double2(c.rr * (c.nu - d.x.x), c.rr * (c.nu - d.x.y));
             k.cw = make_double2(c.rr * (c.nu - d.y.x), c.rr * (c.nu - d.y.y));
             k.cs = make_double2(c.rr * (d.x.x + c.nu), c.rr * (d.x.y + c.nu));
@@ -383,22 +337,30 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             const double2 f = rd[iR].r;
             const bool inr = !GS || (r >= 1 && r <= n - 1);
             if (cs == 0) {
-                const double uW = nbw(ur[iR].y, iR);
+                const double uW = dpp_shr1(ur[iR].y);
                 if (!GS || (inr && in0))
-                    ur[iR].x = div_diag<!GS>(f.x - k.cn.x * ur[iN].x - k.cw.x * uW -
-                                                 k.cs.x * ur[iS].x - k.ce.x * ur[iR].y,
-                                             c);
+                    ur[iR].x = FM ? fm_upd(f.x, k.cn.x, ur[iN].x, k.cw.x, uW, k.cs.x, ur[iS].x,
+                                           k.ce.x, ur[iR].y)
+                                  : div_diag<!GS>(f.x - k.cn.x * ur[iN].x - k.cw.x * uW -
+                                                      k.cs.x * ur[iS].x - k.ce.x * ur[iR].y,
+                                                  c);
             } else {
-                const double uE = nbe(ur[iR].x, iR);
+                const double uE = dpp_shl1(ur[iR].x);
                 if (!GS || (inr && in1))
-                    ur[iR].y = div_diag<!GS>(f.y - k.cn.y * ur[iN].y - k.cw.y * ur[iR].x -
-                                                 k.cs.y * ur[iS].y - k.ce.y * uE,
-                                             c);
+                    ur[iR].y = FM ? fm_upd(f.y, k.cn.y, ur[iN].y, k.cw.y, ur[iR].x, k.cs.y,
+                                           ur[iS].y, k.ce.y, uE)
+                                  : div_diag<!GS>(f.y - k.cn.y * ur[iN].y - k.cw.y * ur[iR].x -
+                                                      k.cs.y * ur[iS].y - k.ce.y * uE,
+                                                  c);
             }
         };
-        // residual (gs.cpp:75 term order) at column c0 of the row in slot iR
+        // residual (gs.cpp:75 term order) at column c0 of the row in slot iR,
+        // from its coefficients
         auto res_x = [&](const int iR, const int iN, const int iS, const double uW) {
             const CoefRow &k = cf[iR];
+            if (FM)
+                return fm_res(rd[iR].r.x, ur[iR].x, k.cn.x, ur[iN].x, k.cw.x, uW, k.cs.x,
+                              ur[iS].x, k.ce.x, ur[iR].y, c);
             return rd[iR].r.x - (c.dgs * ur[iR].x + k.cn.x * ur[iN].x + k.cw.x * uW +
                                  k.cs.x * ur[iS].x + k.ce.x * ur[iR].y);
         };
@@ -421,7 +383,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                     const int s = s0 + it + (p & 1);
                     ur[(p + 3) % NR] = make_u(s + 3, up[(p + 3) % NR], (p + 3) & 1);
                     load_u(s + 3 + XU, up[(p + 3 + XU) % NR], (p + 3 + XU) & 1);   // XU ahead
-                    make_t((p + 1) % NR);   // row s+1: first used by stage 0 below
+                    first_use((p + 1) % NR);   // row s+1: first used by stage 0 below
                     if (XACOEF) {
                         // the row's four coefficients once (as B does), not in
                         // each of its point's stages
@@ -430,7 +392,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         for (int h = 0; h < S; ++h) stage_c(p, h, s + 1 - h);
                     } else {
 #pragma unroll
-                        for (int h = 0; h < S; ++h) stage(ur, rd, p, h, s + 1 - h);
+                        for (int h = 0; h < S; ++h) stage(p, h, s + 1 - h);
                     }
                     // hand-off: rhs/v row s+1 (first used above), final u row s+2-S
                     {
@@ -444,8 +406,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         const int ro = s + 2 - S;
                         const double2 uf = ur[(p + 2 - S + 2 * NR) % NR];
                         uring[pr][(p + 2 - S + 2 * NR) % NU][l] = uf;
-                        st2_ifu(upost + rowoff(ro, ip), c0, post && own(ro),
-                               uf);
+                        st2_ifu(upost + rowoff(ro, ip), c0, post && own(ro), uf);
                     }
                     // residual norm of u_post (multigrid.cpp:112-113), column c0 of
                     // row s+1-S (its neighbours are final now; B takes column c0+1:
@@ -455,24 +416,11 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         const int iR = (p + 1 - S + 2 * NR) % NR;
                         const int iN = (p - S + 2 * NR) % NR;
                         const int iS = (p + 2 - S + 2 * NR) % NR;
-                        const RowData &d = rd[iR];
-                        const double uW = nbw(ur[iR].y, iR);
+                        const double uW = dpp_shr1(ur[iR].y);
                         // (with the row's coefficients: the same expressions, bitwise)
-                        // XG: the row's rhs / t1 / t2 from the hand-off ring
-                        // (B takes them two steps later) and the coefficients
-                        // formed here -- 8 fp64 ops more, but A keeps neither
-                        // the row's coefficients nor its rhs for this step: 20
-                        // VGPRs fewer on A's path, which sets the kernel's count
                         auto res0 = [&]() {
-                            if (XG) {
-                                double2(*slot)[64] = rdring[pr][(p + 1 - S + 2 * NRD) % NRD];
-                                const double2 fr = slot[0][l], f1 = slot[1][l], f2 = slot[2][l];
-                                return res_point_t(fr.x, f1.x, f2.x, ur[iR].x, ur[iN].x, uW,
-                                                   ur[iS].x, ur[iR].y, c);
-                            }
                             if (XACOEF) return res_x(iR, iN, iS, uW);
-                            return res_point_t(d.r.x, d.x.x, d.y.x, ur[iR].x, ur[iN].x, uW,
-                                               ur[iS].x, ur[iR].y, c);
+                            return res_tx(iR, iN, iS, uW);
                         };
                         if (GN) {
                             if (own(r) && r >= 1 && r <= n - 1 && in0) {
@@ -485,9 +433,8 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         }
                     }
                     load_rv(s + XRV, (p + XRV) % NR);
-                    post_edges(ur, p);
-                    if (XG || (p & 1)) __syncthreads();
                     if (p & 1) {   // end of a pair (compile-time)
+                        __syncthreads();
                         it += 2;
                         if (it >= iters) goto done_a;
                     }
@@ -515,18 +462,14 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                     {
                         const int r = s + 2;
                         const int iR = (q + 2) % NR, iN = (q + 1) % NR, iS = (q + 3) % NR;
-                        const RowData &d = rd[iR];
-                        const double uE = nbe(ur[iR].x, iR);
+                        const double uE = dpp_shl1(ur[iR].x);
                         if (GN) {
                             if (own(r) && r >= 1 && r <= n - 1 && in1) {
-                                const double res =
-                                    res_point_t(d.r.y, d.x.y, d.y.y, ur[iR].y, ur[iN].y,
-                                                ur[iR].x, ur[iS].y, uE, c);
+                                const double res = res_ty(iR, iN, iS, uE);
                                 acc += res * res;
                             }
                         } else {   // acc + 0.0 == acc (acc >= +0): a select, no branch
-                            const double r1 = res_point_t(d.r.y, d.x.y, d.y.y, ur[iR].y,
-                                                          ur[iN].y, ur[iR].x, ur[iS].y, uE, c);
+                            const double r1 = res_ty(iR, iN, iS, uE);
                             acc += own(r) ? r1 * r1 : 0.0;
                         }
                     }
@@ -535,11 +478,11 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         // (gs.cpp:44), stored on the owned interior points, and the
                         // residual of u_post against it (multigrid.cpp:104); it
                         // replaces this step's rhs in the ring for B's stages and
-                        // restriction
+                        // restriction (FM: scaled to f/d after)
                         const int r = s + 2;
                         const int iR = (q + 2) % NR, iN = (q + 1) % NR, iS = (q + 3) % NR;
                         RowData &d = rd[iR];
-                        const double uW = nbw(ur[iR].y, iR), uE = nbe(ur[iR].x, iR);
+                        const double uW = dpp_shr1(ur[iR].y), uE = dpp_shl1(ur[iR].x);
                         Coef cg = c;   // fresh nu: no coefficient CSE into the stages
                         asm volatile("" : "+s"(cg.nu));
                         const double f0 = rhs_point_t(d.x.x, d.y.x, ur[iR].x, ur[iN].x, uW,
@@ -564,6 +507,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                                                       ur[iR].x, ur[iS].y, uE, cg);
                         acc2 += (own(r) && i0) ? e0 * e0 : 0.0;
                         acc2 += (own(r) && i1) ? e1 * e1 : 0.0;
+                        if (FM) d.r = make_double2(f0 * c.rdgs, f1 * c.rdgs);
                     }
                     to_coef(rd[(q + 1) % NR], cf[(q + 1) % NR]);   // row s+1
 #pragma unroll
@@ -571,7 +515,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                     {
                         const int ro = s + 2 - S;
                         st2_ifu(upre + rowoff(ro, ip), c0, own(ro),
-                               ur[(q + 2 - S + 2 * NR) % NR]);
+                                ur[(q + 2 - S + 2 * NR) % NR]);
                     }
                     if (((q + 1 - S) & 1) == 0) {   // compile-time row parity
                         // residual -> coarse rhs at the even-even points (:73-75)
@@ -579,15 +523,14 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         const int iR = (q + 1 - S + 2 * NR) % NR;
                         const int iN = (q - S + 2 * NR) % NR;
                         const int iS = (q + 2 - S + 2 * NR) % NR;
-                        const double uW = nbw(ur[iR].y, iR);
+                        const double uW = dpp_shr1(ur[iR].y);
                         const bool on = own(r) &&
                                         (!GN || (r >= 1 && r <= n - 2 && in0 && c0 <= n - 2));
                         const double res = res_x(iR, iN, iS, uW);
                         st1_ifu(rhsc + rowoff(r >> 1, ipc), c0 >> 1, on, res);
                     }
-                    post_edges(ur, q);
-                    if (XG || (p & 1)) __syncthreads();
                     if (p & 1) {
+                        __syncthreads();
                         it += 2;
                         if (it >= iters) goto done_b;
                     }
@@ -603,19 +546,8 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
         start += b - a;
         // a pair past its region's strips idles on the segment (A and B alike,
         // so each pair's barrier count still matches between its two waves)
-        if (__builtin_amdgcn_readfirstlane(strip) >= 0) {
-            if (XG) {
-                // group g = strips g*WPB .. g*WPB+WPB-1 (regions start at a
-                // multiple of WPB, so strip % WPB == pr); the last group is
-                // shifted left to end at xend and owns only what is left
-                const int g = strip / WPB;
-                const int k0 = xg.x0 + g * WGc;
-                const int og = g < xg.glast ? k0 : xg.xl;
-                march(og - 2 * H + 128 * pr, k0, g < xg.glast ? k0 + WGc : xg.xend, a, b);
-            } else {
-                march(strip * W - 2 * H, strip * W, strip * W + W, a, b);
-            }
-        }
+        if (__builtin_amdgcn_readfirstlane(strip) >= 0)
+            march(strip * W - 2 * H, strip * W, strip * W + W, a, b);
     }
     const double tot = wave_sum(acc);   // one partial per wave (A: columns c0, B: c0+1)
     if (l == 0) partials[(long)blockIdx.x * 2 * WPB + wv] = tot;
@@ -684,7 +616,9 @@ struct PtCoef {
     double f, cn, cw, cs, ce;
 };
 
-template <int K, int TRV>
+// FM: fp_mode fma (stencil.h): the pair keeps f' = f/d and the m = -c/d of
+// the contracted update instead.
+template <int K, int TRV, bool FM>
 __global__ __launch_bounds__(256) void k_xtile(
     const double *__restrict__ uin, double *__restrict__ uout, double *__restrict__ upost,
     const double *__restrict__ rhs, const double *__restrict__ v1, const double *__restrict__ v2,
@@ -748,8 +682,17 @@ __global__ __launch_bounds__(256) void k_xtile(
             }
             const double2 rr = ld2(rhs + o), xx = ld2(v1 + o), yy = ld2(v2 + o);
             // gs.cpp:126-129: aa, bb from v2 (W / E), cc, dd from v1 (N / S)
-            const PtCoef X{rr.x, coef_a(xx.x, c), coef_a(yy.x, c), coef_b(xx.x, c), coef_b(yy.x, c)};
-            const PtCoef Y{rr.y, coef_a(xx.y, c), coef_a(yy.y, c), coef_b(xx.y, c), coef_b(yy.y, c)};
+            const double hh = c.h * 0.5;   // FM: from t = v*h/2 (stencil.h)
+            const PtCoef X =
+                FM ? PtCoef{rr.x * c.rdgs, fm_mp(xx.x * hh, c), fm_mp(yy.x * hh, c),
+                            fm_mm(xx.x * hh, c), fm_mm(yy.x * hh, c)}
+                   : PtCoef{rr.x, coef_a(xx.x, c), coef_a(yy.x, c), coef_b(xx.x, c),
+                            coef_b(yy.x, c)};
+            const PtCoef Y =
+                FM ? PtCoef{rr.y * c.rdgs, fm_mp(xx.y * hh, c), fm_mp(yy.y * hh, c),
+                            fm_mm(xx.y * hh, c), fm_mm(yy.y * hh, c)}
+                   : PtCoef{rr.y, coef_a(xx.y, c), coef_a(yy.y, c), coef_b(xx.y, c),
+                            coef_b(yy.y, c)};
             P0[m] = par ? Y : X;
             P1[m] = par ? X : Y;
 #pragma unroll
@@ -780,7 +723,8 @@ __global__ __launch_bounds__(256) void k_xtile(
                 const PtCoef &P = (h & 1) ? P1[m] : P0[m];
                 const double uN = ot[q - HW], uS = ot[q + HW];
                 const double uW = ot[q - 1 + cs], uE = ot[q + cs];
-                ow[q] = div_diag(P.f - P.cn * uN - P.cw * uW - P.cs * uS - P.ce * uE, c);
+                ow[q] = FM ? fm_upd(P.f, P.cn, uN, P.cw, uW, P.cs, uS, P.ce, uE)
+                           : div_diag(P.f - P.cn * uN - P.cw * uW - P.cs * uS - P.ce * uE, c);
             }
             __syncthreads();
         }
@@ -793,6 +737,9 @@ __global__ __launch_bounds__(256) void k_xtile(
         const double *pu = tu + pl * PL, *ot = tu + (pl ^ 1) * PL;
         const PtCoef &P = even_pt ? P0[m] : P1[m];
         // gs.cpp:75: rhs - (d*u + cc*uN + aa*uW + dd*uS + bb*uE)
+        if (FM)
+            return fm_res(P.f, pu[q], P.cn, ot[q - HW], P.cw, ot[q - 1 + cs], P.cs, ot[q + HW],
+                          P.ce, ot[q + cs], c);
         return P.f - (c.dgs * pu[q] + P.cn * ot[q - HW] + P.cw * ot[q - 1 + cs] +
                       P.cs * ot[q + HW] + P.ce * ot[q + cs]);
     };
@@ -857,7 +804,7 @@ long g_xfast = 1;   // unguarded interior march kernels (tuning key "xfast")
 void set_xfast(long v) { g_xfast = v; }
 long get_xfast() { return g_xfast; }
 
-template <int WPB, int K, bool G, bool RS = false, bool SV = false, bool XG = false>
+template <int WPB, int K, bool G, bool RS, bool SV, bool FM>
 static int xsmooth_slots() {
     static int slots = 0;   // resident workgroups of this instantiation
     if (!slots) {
@@ -865,7 +812,7 @@ static int xsmooth_slots() {
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per,
-                                                           k_xsmooth<WPB, K, G, RS, SV, XG>,
+                                                           k_xsmooth<WPB, K, G, RS, SV, FM>,
                                                            128 * WPB, 0);
         slots = std::max(1, cus) * std::max(1, per);
     }
@@ -874,78 +821,43 @@ static int xsmooth_slots() {
 
 // One launch over `reg`; min_rows: the fewest rows per workgroup (each
 // workgroup's march pays a warm-up of ~EA + EB + D rows).  Returns the norm
-// partials written (grid * 2 * WPB: one per wave) at `partials`.  geo: the
-// group geometry (XG) or the guarded kernel's excluded rectangle.
-template <int WPB, int K, bool G, bool RS, bool SV, bool XG>
+// partials written (grid * 2 * WPB: one per wave) at `partials`.
+template <int WPB, int K, bool G, bool RS, bool SV, bool FM>
 static int xsmooth_launch_sv(const XArgs &A, const MarchRegions &reg, double *partials, int lo,
-                             int hi, long min_rows, long max_wgs, const XGeo &geo,
-                             hipStream_t s) {
+                             int hi, long min_rows, long max_wgs, hipStream_t s) {
     const long total = reg.pre[reg.count];
     if (total <= 0) return 0;
     long upw;
     MarchRegions r;
     using X = XCfg<K>;
-    const unsigned grid = plan_march(reg, WPB, xsmooth_slots<WPB, K, G, RS, SV, XG>(), min_rows,
+    const unsigned grid = plan_march(reg, WPB, xsmooth_slots<WPB, K, G, RS, SV, FM>(), min_rows,
                                      max_wgs, X::EA + X::EB + X::D + X::NR / 2, upw, r);
     // RS: the second partials (the next step's initial norm) at the same
     // offsets, kNormBlocks further on
-    MGX_LAUNCH((k_xsmooth<WPB, K, G, RS, SV, XG>), dim3(grid), dim3(128 * WPB), s, A.uin,
+    MGX_LAUNCH((k_xsmooth<WPB, K, G, RS, SV, FM>), dim3(grid), dim3(128 * WPB), s, A.uin,
                A.upost, A.upre, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n,
                A.pitch, r, upw, A.c, lo, hi, A.store_post ? 1 : 0, A.rhs_next,
-               RS ? partials + kNormBlocks : (double *)nullptr, A.sa1, A.sb1, A.sa2, A.sb2, geo);
+               RS ? partials + kNormBlocks : (double *)nullptr, A.sa1, A.sb1, A.sa2, A.sb2);
     return (int)grid * 2 * WPB;
 }
-// SV when the level's velocity factors are given (XArgs::sa1)
-template <int WPB, int K, bool G, bool RS = false, bool XG = false>
+// SV when the level's velocity factors are given (XArgs::sa1); FM = the
+// level's fp_mode (Coef::fm)
+template <int WPB, int K, bool G, bool RS = false>
 static int xsmooth_launch(const XArgs &A, const MarchRegions &reg, double *partials, int lo, int hi,
-                          long min_rows, long max_wgs, hipStream_t s,
-                          const XGeo &geo = XGeo{0, 0, 0, 0, 0, 0, 0, 0}) {
-    if (A.sa1 && A.sb1 && A.sa2 && A.sb2)
-        return xsmooth_launch_sv<WPB, K, G, RS, true, XG>(A, reg, partials, lo, hi, min_rows,
-                                                          max_wgs, geo, s);
-    return xsmooth_launch_sv<WPB, K, G, RS, false, XG>(A, reg, partials, lo, hi, min_rows,
-                                                       max_wgs, geo, s);
-}
-
-// tuning key "xgroup": the group-exchange interior kernel (XG), default off:
-// bitwise, 13 % less VALU per owned point (28 halo columns per 512 instead of
-// per 128), but level 0 2.09 vs 1.88 ms at N=16384 -- the per-step barrier
-// and the exchange reads' LDS latency on every stage chain (at 250 VGPRs the
-// reads cannot be issued ahead) cost more than the halo work saved
-long g_xgroup = 0;
-void set_xgroup(long v) { g_xgroup = v; }
-long get_xgroup() { return g_xgroup; }
-
-// The XG launch's work: groups of WPB strips, each owning WGc = 128 WPB - 4H
-// columns, group 0 from column x0 = 2H + 2 (lane 0 on column 2, even), the
-// last group shifted left so that its last lane is column n-1 (owning what
-// the others leave up to xend), x rows [ma, mb); and the guarded kernel's
-// work around it in W-column strips: the strips holding columns [0, x0) and
-// [xend, n] on all rows, the others on the rows outside [ma, mb), with the
-// XG launch's rectangle excluded (XGeo::ec0..er1).  false: no group fits.
-template <int WPB, int K>
-static bool xg_regions(long n, int ra, int rb, int top, int bot, MarchRegions &inner,
-                       MarchRegions &edge, XGeo &geo) {
-    using X = XCfg<K>;
-    // the XG march starts 2 rows earlier (k_xsmooth): 2 more margin rows
-    const int ma = std::max(ra, top + 2), mb = std::min(rb, (int)n + 1 - bot);
-    constexpr int H = X::H, W = X::W, WGc = 128 * WPB - 4 * H;
-    inner = MarchRegions{};
-    edge = MarchRegions{};
-    const int x0 = 2 * H + 2;
-    const long xl = (n + 2 * H - 128 * WPB) & ~1L;
-    if (xl < x0 || mb <= ma) return false;
-    const int xend = (int)xl + WGc;
-    const int groups = (xend - x0 + WGc - 1) / WGc;
-    geo = XGeo{x0, (int)xl, xend, groups - 1, x0, xend, ma, mb};
-    add_region<WPB>(inner, 0, groups * WPB, ma, mb);
-    const int strips = (int)((n + 1 + W - 1) / W);
-    const int sl = (x0 + W - 1) / W, sr = std::min(strips, xend / W);
-    add_region<1>(edge, 0, sl, ra, rb);
-    add_region<1>(edge, sr, strips, ra, rb);
-    add_region<1>(edge, sl, sr, ra, ma);
-    add_region<1>(edge, sl, sr, mb, rb);
-    return true;
+                          long min_rows, long max_wgs, hipStream_t s) {
+    const bool sv = A.sa1 && A.sb1 && A.sa2 && A.sb2;
+    if (A.c.fm) {
+        if (sv)
+            return xsmooth_launch_sv<WPB, K, G, RS, true, true>(A, reg, partials, lo, hi,
+                                                               min_rows, max_wgs, s);
+        return xsmooth_launch_sv<WPB, K, G, RS, false, true>(A, reg, partials, lo, hi, min_rows,
+                                                            max_wgs, s);
+    }
+    if (sv)
+        return xsmooth_launch_sv<WPB, K, G, RS, true, false>(A, reg, partials, lo, hi, min_rows,
+                                                            max_wgs, s);
+    return xsmooth_launch_sv<WPB, K, G, RS, false, false>(A, reg, partials, lo, hi, min_rows,
+                                                         max_wgs, s);
 }
 
 static void add_tile_region(TileRegions &r, int c0, int c1, int r0, int r1, int TR) {
@@ -981,6 +893,19 @@ static void xmargins(const XArgs &A, int ra, int rb, int &top, int &bot) {
     bot = std::max(X::BOT, (int)A.n + 1 - rb + A.band);
 }
 
+template <int K, int TRV>
+static void xtile_launch(const XArgs &A, const TileRegions &t, int tiles, double *partials, int lo,
+                         int hi, hipStream_t s) {
+    if (A.c.fm)
+        MGX_LAUNCH((k_xtile<K, TRV, true>), dim3((unsigned)tiles), dim3(256), s, A.uin, A.upre,
+                   A.upost, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch,
+                   t, A.c, lo, hi, A.store_post ? 1 : 0);
+    else
+        MGX_LAUNCH((k_xtile<K, TRV, false>), dim3((unsigned)tiles), dim3(256), s, A.uin, A.upre,
+                   A.upost, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch,
+                   t, A.c, lo, hi, A.store_post ? 1 : 0);
+}
+
 template <int WPB, int K>
 static int xsmooth_tiled(const XArgs &A, int ra, int rb, int lo, int hi, hipStream_t s) {
     using X = XCfg<K>;
@@ -989,14 +914,10 @@ static int xsmooth_tiled(const XArgs &A, int ra, int rb, int lo, int hi, hipStre
     xmargins<K>(A, ra, rb, top, bot);
     march_split(n, X::W, X::H, ra, rb, top, bot, si0, si1, ma, mb);
     TileRegions t{};
-    MarchRegions ginner, gedge;
-    XGeo geo{};
-    const bool xg = g_xgroup != 0 && xg_regions<WPB, K>(n, ra, rb, top, bot, ginner, gedge, geo);
-    if (xg) ma = geo.er0;   // the XG march's rows: [er0, er1)
-    const bool inner_march = (xg || si1 > si0) && mb - ma >= kXTileAllRows;
+    const bool inner_march = si1 > si0 && mb - ma >= kXTileAllRows;
     if (inner_march) {
-        const int ca = xg ? geo.x0 : si0 * X::W;
-        const int cb = xg ? geo.xend : (int)std::min<long>(n + 1, (long)si1 * X::W);
+        const int ca = si0 * X::W;
+        const int cb = (int)std::min<long>(n + 1, (long)si1 * X::W);
         add_tile_region(t, 0, ca, ra, rb, kXTileRows);
         add_tile_region(t, cb, (int)n + 1, ra, rb, kXTileRows);
         add_tile_region(t, ca, cb, ra, ma, kXTileRows);
@@ -1009,22 +930,13 @@ static int xsmooth_tiled(const XArgs &A, int ra, int rb, int lo, int hi, hipStre
     if (tiles > kNormBlocks / 2) return -2;   // too many: the caller marches the edges
     int pm = A.phase == 2 ? A.partials_done : 0;
     if (inner_march && A.phase != 2) {
-        if (xg) {
-            pm = xsmooth_launch<WPB, K, false, false, true>(A, ginner, A.partials, lo, hi,
-                                                            A.min_rows,
-                                                            kNormBlocks / (2 * WPB) / 2, s, geo);
-        } else {
-            MarchRegions inner{};
-            add_region<WPB>(inner, si0, si1, ma, mb);
-            pm = xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, A.min_rows,
-                                               kNormBlocks / (2 * WPB) / 2, s);
-        }
+        MarchRegions inner{};
+        add_region<WPB>(inner, si0, si1, ma, mb);
+        pm = xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, A.min_rows,
+                                           kNormBlocks / (2 * WPB) / 2, s);
     }
     if (A.phase == 1) return pm;
-    if (tiles > 0)
-        MGX_LAUNCH((k_xtile<K, kXTileRows>), dim3((unsigned)tiles), dim3(256), s, A.uin, A.upre,
-                   A.upost, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, A.partials + pm, (int)n,
-                   A.pitch, t, A.c, lo, hi, A.store_post ? 1 : 0);
+    if (tiles > 0) xtile_launch<K, kXTileRows>(A, t, tiles, A.partials + pm, lo, hi, s);
     return pm + tiles;
 }
 
@@ -1048,8 +960,6 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
         if (g_xfast == 0 || !(A.c.dgs > 0) || A.rb >= 0 || rb - ra <= g_xtile_max_rows)
             return -3;
         MarchRegions inner, edge, unused;
-        // (the time-step mode keeps the separate strips: its B wave's extra
-        // stage takes the XG kernel past 256 VGPRs)
         march_regions<WPB>(n, X::W, X::H, ra, rb, X::TOP_RS, X::BOT, true, inner, unused);
         march_regions<1>(n, X::W, X::H, ra, rb, X::TOP_RS, X::BOT, true, unused, edge);
         const int pm = xsmooth_launch<WPB, K, false, true>(A, inner, A.partials, lo, hi,
@@ -1074,24 +984,16 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
     }
     int top, bot;
     xmargins<K>(A, ra, rb, top, bot);
-    XGeo geo{};
-    const bool xg =
-        split && g_xgroup != 0 && xg_regions<WPB, K>(n, ra, rb, top, bot, inner, edge, geo);
-    if (!xg) {
-        march_regions<WPB>(n, X::W, X::H, ra, rb, top, bot, split, inner, unused);
-        march_regions<1>(n, X::W, X::H, ra, rb, top, bot, split, unused, edge);
-    }
+    march_regions<WPB>(n, X::W, X::H, ra, rb, top, bot, split, inner, unused);
+    march_regions<1>(n, X::W, X::H, ra, rb, top, bot, split, unused, edge);
     int pm = A.partials_done;
     if (A.phase != 2)
-        pm = xg ? xsmooth_launch<WPB, K, false, false, true>(A, inner, A.partials, lo, hi,
-                                                             A.min_rows,
-                                                             kNormBlocks / (2 * WPB) / 2, s, geo)
-                : xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, A.min_rows,
-                                                kNormBlocks / (2 * WPB) / 2, s);
+        pm = xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, A.min_rows,
+                                           kNormBlocks / (2 * WPB) / 2, s);
     if (A.phase == 1) return pm;
     const int pe = xsmooth_launch<1, K, true>(A, edge, A.partials + pm, lo, hi,
                                               std::min(MGX_XEDGE_ROWS, A.min_rows),
-                                              kNormBlocks / 2 / 2, s, geo);
+                                              kNormBlocks / 2 / 2, s);
     return pm + pe;
 }
 

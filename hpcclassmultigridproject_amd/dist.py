@@ -87,10 +87,12 @@ def rccl_selfcheck(world: int, rank: int, device: int, n: int = 4096, maxlvl: in
     count) and runs ``cycles`` V-cycles with it -- ghost send/recv, the
     all-gather into the replicated levels, the norm all-reduce, the
     all-gather + broadcast of the download -- once with the exchanges on the
-    compute stream and once overlapped (``dist_overlap``); rank 0 compares u
-    bitwise and the norms to 1e-11 with a one-GPU context.  Collective over
+    compute stream and overlapped (``dist_overlap`` 0 / 1 / 2), in both
+    arithmetic modes; rank 0 compares u bitwise and the norms to 1e-11 with a
+    one-GPU context of the same fp_mode.  Collective over
     the torch.distributed group (its backend only brokers the unique ids and
-    the verdict).  -> {"bitwise": bool, "norm_rel_err": float, ...} on every rank.
+    the verdict).  -> {"bitwise": bool, "norm_rel_err": float, "modes": {overlap:
+    {...}}, ...} on every rank.
     """
     import numpy as np
     import torch
@@ -101,40 +103,55 @@ def rccl_selfcheck(world: int, rank: int, device: int, n: int = 4096, maxlvl: in
     dt, nu = 1.0 / n / 10, -4e-4
     u0, v1, v2 = init_problem(n)
     old_rows, old_ov = _lib.get_tuning("dist_min_rows"), _lib.get_tuning("dist_overlap")
-    ref = None
+    fps = {"bitwise": _lib.FP_BITWISE, "fma": _lib.FP_FMA}
+    ref = {}
     if rank == 0:
-        with Multigrid(n, maxlvl, dt, nu, device=device) as mg:
-            mg.upload(u0, v1, v2)
-            mg.rhs()
-            ref = ([mg.run_cycles(1) for _ in range(cycles)], mg.download())
-    ok, err, la = True, 0.0, None
+        for name, fp in fps.items():
+            with Multigrid(n, maxlvl, dt, nu, device=device, fp_mode=fp) as mg:
+                mg.upload(u0, v1, v2)
+                mg.rhs()
+                ref[name] = ([mg.run_cycles(1) for _ in range(cycles)], mg.download())
+    # per dist_overlap mode: [bitwise so far (both fp modes), max norm error]
+    modes, la = {}, None
     try:
         _lib.set_tuning("dist_min_rows", 16)
         for ov in (0, 1, 2):
             _lib.set_tuning("dist_overlap", ov)
-            uid = broadcast_unique_id(group)
-            with Multigrid(n, maxlvl, dt, nu, device=device, world=world, rank=rank,
-                           unique_id=uid) as mg:
-                la = mg.dist_info()[2]
-                mg.upload(u0, v1, v2)
-                mg.profile(True, finest_only=True)
-                mg.rhs()
-                norms = [mg.run_cycles(1) for _ in range(cycles)]
-                # the cross-cycle pass (and so the overlapped exchange) really ran
-                ok = ok and mg.profile_get(_lib.K_XSMOOTH, 0)[0] > 0
-                u = mg.download()
-            if rank == 0:
-                ok = ok and bool(np.array_equal(u, ref[1]))
-                err = max(err, float(np.max(np.abs(np.array(norms) - ref[0]) /
-                                            np.abs(ref[0]))))
+            ok, err = True, 0.0
+            for name, fp in fps.items():
+                uid = broadcast_unique_id(group)
+                with Multigrid(n, maxlvl, dt, nu, device=device, world=world, rank=rank,
+                               unique_id=uid, fp_mode=fp) as mg:
+                    la = mg.dist_info()[2]
+                    mg.upload(u0, v1, v2)
+                    mg.profile(True, finest_only=True)
+                    mg.rhs()
+                    norms = [mg.run_cycles(1) for _ in range(cycles)]
+                    # the cross-cycle pass (and so the overlapped exchange) really ran
+                    ok = ok and mg.profile_get(_lib.K_XSMOOTH, 0)[0] > 0
+                    u = mg.download()
+                if rank == 0:
+                    # u bitwise the one-GPU context's of the same fp mode (the
+                    # fma forms do not depend on the partition either)
+                    ok = ok and bool(np.array_equal(u, ref[name][1]))
+                    err = max(err, float(np.max(np.abs(np.array(norms) - ref[name][0]) /
+                                                np.abs(ref[name][0]))))
+            modes[ov] = [ok, err]
     finally:
         _lib.set_tuning("dist_min_rows", old_rows)
         _lib.set_tuning("dist_overlap", old_ov)
-    verdict = torch.tensor([1.0 if ok else 0.0, err], dtype=torch.float64)
+    verdict = torch.tensor([x for ov in (0, 1, 2) for x in (1.0 if modes[ov][0] else 0.0,
+                                                             modes[ov][1])],
+                           dtype=torch.float64)
     if dist.get_backend(group) == "nccl":
         verdict = verdict.cuda()
     dist.broadcast(verdict, src=0, group=group)
-    ok, err = bool(verdict[0].item() == 1.0), float(verdict[1].item())
+    v = verdict.cpu().tolist()
+    per = {str(ov): {"bitwise": v[2 * k] == 1.0, "norm_rel_err": v[2 * k + 1],
+                     "passed": v[2 * k] == 1.0 and v[2 * k + 1] <= 1e-11}
+           for k, ov in enumerate((0, 1, 2))}
     return {"N": n, "levels": maxlvl, "cycles": cycles, "partitioned_levels": la,
-            "overlap": [0, 1, 2], "bitwise": ok, "norm_rel_err": err,
-            "passed": ok and err <= 1e-11}
+            "fp_modes": list(fps), "overlap": [0, 1, 2], "modes": per,
+            "bitwise": all(m["bitwise"] for m in per.values()),
+            "norm_rel_err": max(m["norm_rel_err"] for m in per.values()),
+            "passed": all(m["passed"] for m in per.values())}

@@ -49,11 +49,12 @@ def init_problem_rows(N: int, r0: int, r1: int, nthreads: int = 0):
 
 
 def timestepper(uT, u0, v1, v2, nu, maxlvl, n, dt, T, dx, tol, shape=1, *, nsmooth=3,
-                tower_mode=_lib.TOWER_REFERENCE, device=-1):
+                tower_mode=_lib.TOWER_REFERENCE, device=-1, fp_mode=_lib.FP_BITWISE):
     """multigrid.cpp:124 -- run (int)(T/dt) CN steps; writes uT, returns cycles per step."""
     steps = int(T / dt)
     cyc = (C.c_int * max(steps, 1))()
-    opt = default_options(shape=shape, nsmooth=nsmooth, tower_mode=tower_mode, device=device)
+    opt = default_options(shape=shape, nsmooth=nsmooth, tower_mode=tower_mode, device=device,
+                          fp_mode=fp_mode)
     check(lib().mgx_timestepper_ex(_np_ptr(uT), _np_ptr(u0), _np_ptr(v1), _np_ptr(v2), nu,
                                    maxlvl, n, dt, T, dx, tol, C.byref(opt), cyc))
     return list(cyc)[:steps]
@@ -83,12 +84,13 @@ class Multigrid:
     def __init__(self, N, maxlvl, dt, nu, *, nsmooth=3, shape=1,
                  tower_mode=_lib.TOWER_REFERENCE, device=-1, smoother=0, fuse=3,
                  coarse_tol=1e-5, coarse_maxit=1000, max_cycle=50,
-                 world=1, rank=0, unique_id=None, local_parts=0):
+                 world=1, rank=0, unique_id=None, local_parts=0, fp_mode=_lib.FP_BITWISE):
         self.N, self.maxlvl, self.dt, self.nu = N, maxlvl, dt, nu
         self.opt = default_options(nsmooth=nsmooth, shape=shape, tower_mode=tower_mode,
                                    device=device, smoother=smoother, fuse=fuse,
                                    coarse_tol=coarse_tol,
-                                   coarse_maxit=coarse_maxit, max_cycle=max_cycle)
+                                   coarse_maxit=coarse_maxit, max_cycle=max_cycle,
+                                   fp_mode=fp_mode)
         h = C.c_void_p()
         if local_parts:
             check(lib().mgx_create_local_dist(C.byref(h), N, maxlvl, dt, nu,

@@ -18,7 +18,8 @@
  *     null-stream work; mgx_compute_norm synchronises (it returns a host value,
  *     like gs.cpp:86).  Context functions run on the context's own stream;
  *   - all arithmetic is fp64 with the reference's term order and no FMA
- *     contraction, so op results are bitwise equal to the serial reference.
+ *     contraction, so op results are bitwise equal to the serial reference
+ *     (a context may opt into contracted smoothing passes: MGX_FP_FMA).
  */
 #ifndef MGX_H
 #define MGX_H
@@ -91,7 +92,23 @@ typedef struct mgx_options {
                            (default); 1 = two in-place colour passes per sweep;
                            2 = one-pass single sweeps (no temporal blocking) */
     int fuse;           /* smoother 0: max RB sweeps per HBM pass, 1..3 (default 3) */
+    int fp_mode;        /* MGX_FP_BITWISE (default) or MGX_FP_FMA, below */
 } mgx_options;
+
+/* Arithmetic of the smoothing passes (smoother 0: the fused row marches,
+ * LDS tiles and the coarsest solve; the gs.h mirror ops, smoothers 1/2 and
+ * compute_rhs are always bitwise).
+ * MGX_FP_BITWISE: the reference's expressions term by term, no contraction,
+ *   the correctly rounded division -- u bitwise equal to the serial reference.
+ * MGX_FP_FMA: the operator divided by its diagonal and contracted: each
+ *   update u = f/d + m_N uN + m_W uW + m_E uE + m_S uS as four fused
+ *   multiply-adds (m = -coefficient/d), residuals d*(update - u) -- within a
+ *   few ulp per operation of the reference (max|duT| <= 1e-12,
+ *   the same cycle counts), independent of the kernel or row partition that
+ *   computes a point.  The reference's own GPU build contracts too (nvcc
+ *   defaults to -fmad=true, gs.cu). */
+#define MGX_FP_BITWISE 0
+#define MGX_FP_FMA 1
 
 /* Fills *opt with the reference defaults. */
 void mgx_default_options(mgx_options *opt);
@@ -159,11 +176,11 @@ int mgx_stream(mgx_ctx *ctx, void **stream);
 int mgx_synchronize(mgx_ctx *ctx);
 
 /* Process-wide tuning knobs.  "tile_max_n": levels with n <= value run the
- * fused smoothing pass as 2-D LDS tiles instead of the row march (default 1024;
- * env MGX_TILE_MAX_N).
+ * fused smoothing pass as 2-D LDS tiles instead of the row march (default 1024).
  * "cross_cycle": 1 (default) fuses, inside mg_outer / run_cycles / step, the
  * finest level's post-smoothing of each V-cycle with the pre-smoothing of
- * the next into one HBM pass (levels with n >= 4096, V-cycles, nsmooth 2 or
+ * the next into one HBM pass (levels with n >= 4096, V- and W-cycles -- a
+ * W-cycle also fuses its two level-0 visits --, nsmooth 2 or
  * 3; bitwise the same results); after such a cycle the coarse levels hold
  * the next cycle's restricted rhs, not the last correction.  0 = off.
  * "dist_min_rows": partitioned solvers replicate every level whose row blocks
@@ -179,10 +196,6 @@ int mgx_synchronize(mgx_ctx *ctx);
  * "xfast": 1 (default) runs the cross-cycle pass as an unguarded kernel over
  * the interior strips and rows plus a guarded kernel over the boundary strips
  * and bands; 0 = one guarded launch (bitwise the same results).
- * "xgroup": 1 runs that interior kernel as groups of four adjacent 128-column
- * strips exchanging their edge columns through LDS (the halo of the temporal
- * blocking only on the group's outer sides); 0 (default) = independent strips,
- * each with its own halo (bitwise the same results; 0 is faster on MI355X).
  * "march_tile_rows": a row block whose wave march would give each resident
  * workgroup fewer than this many rows runs as LDS tiles (default 16, >= 0).
  * "xtile_max_rows": on row blocks of at most this many rows (a rank of a
@@ -192,8 +205,8 @@ int mgx_synchronize(mgx_ctx *ctx);
  * "march_order": work order of the row marches, bit 0 = band-major (the
  * workgroups of neighbouring strip groups march the same rows at the same
  * time, so their shared halo columns are fetched once; launches with >= 192
- * rows per workgroup), bit 1 = XCD-contiguous workgroup order; default 3
- * (env MGX_MARCH_ORDER).  "tile_xcd": 1 (default) deals the LDS tiles
+ * rows per workgroup), bit 1 = XCD-contiguous workgroup order; default 3.
+ * "tile_xcd": 1 (default) deals the LDS tiles
  * XCD-contiguous.  "tile32_min_n": K=3 tile passes on levels n >= value use
  * 32-row tiles (default 2048).  "march_min_rows": fewest rows per workgroup
  * of a wave-march launch (default 32, >= 8).

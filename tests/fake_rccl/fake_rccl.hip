@@ -50,6 +50,7 @@ const char *kFnNames[kNumFn] = {"ncclCommInitRank", "ncclCommDestroy", "ncclGrou
                                 "ncclAllReduce", "ncclBroadcast", "ncclGetUniqueId",
                                 "ncclCommSplit"};
 std::atomic<long> g_calls[kNumFn];
+thread_local long t_calls[kNumFn];   // the calling thread's (one rank's) calls
 std::atomic<long> g_bytes{0};
 std::mutex g_err_mu;
 std::string g_err;   // first failure, process-wide (read by the test)
@@ -395,6 +396,7 @@ const char *ncclGetErrorString(ncclResult_t r) {
 ncclResult_t ncclGetUniqueId(ncclUniqueId *id) {
     static std::atomic<long> ctr{0};
     g_calls[kUniqueId]++;
+    t_calls[kUniqueId]++;
     if (!id) return bad(ncclInvalidArgument, "null id");
     memset(id, 0, sizeof(*id));
     snprintf(id->internal, sizeof(id->internal), "fake-rccl:%d:%ld", (int)getpid(), ctr++);
@@ -448,6 +450,7 @@ static ncclResult_t init_rank(ncclComm_t *out, int nranks, const std::string &ke
 
 ncclResult_t ncclCommInitRank(ncclComm_t *out, int nranks, ncclUniqueId id, int rank) {
     g_calls[kInit]++;
+    t_calls[kInit]++;
     if (!out || nranks < 1 || rank < 0 || rank >= nranks)
         return bad(ncclInvalidArgument, "ncclCommInitRank: bad args");
     return init_rank(out, nranks, std::string(id.internal, sizeof(id.internal)), rank);
@@ -460,6 +463,7 @@ ncclResult_t ncclCommInitRank(ncclComm_t *out, int nranks, ncclUniqueId id, int 
 ncclResult_t ncclCommSplit(ncclComm_t comm, int color, int key, ncclComm_t *out,
                            ncclConfig_t *config) {
     g_calls[kSplit]++;
+    t_calls[kSplit]++;
     (void)config;
     if (!comm || !out) return bad(ncclInvalidArgument, "ncclCommSplit: bad args");
     if (color != 0 || key != comm->rank)
@@ -470,6 +474,7 @@ ncclResult_t ncclCommSplit(ncclComm_t comm, int color, int key, ncclComm_t *out,
 
 ncclResult_t ncclCommDestroy(ncclComm_t c) {
     g_calls[kDestroy]++;
+    t_calls[kDestroy]++;
     if (!c) return ncclSuccess;
     for (hipEvent_t e : c->events) {
         (void)hipEventSynchronize(e);
@@ -491,12 +496,14 @@ ncclResult_t ncclCommDestroy(ncclComm_t c) {
 
 ncclResult_t ncclGroupStart(void) {
     g_calls[kGroupStart]++;
+    t_calls[kGroupStart]++;
     ++t_depth;
     return ncclSuccess;
 }
 
 ncclResult_t ncclGroupEnd(void) {
     g_calls[kGroupEnd]++;
+    t_calls[kGroupEnd]++;
     if (t_depth <= 0) return bad(ncclInvalidUsage, "ncclGroupEnd without ncclGroupStart");
     if (--t_depth > 0) return ncclSuccess;
     return flush_group();
@@ -505,24 +512,28 @@ ncclResult_t ncclGroupEnd(void) {
 ncclResult_t ncclSend(const void *buf, size_t count, ncclDataType_t t, int peer, ncclComm_t comm,
                       hipStream_t st) {
     g_calls[kSend]++;
+    t_calls[kSend]++;
     return enqueue(true, const_cast<void *>(buf), count, t, peer, comm, st);
 }
 
 ncclResult_t ncclRecv(void *buf, size_t count, ncclDataType_t t, int peer, ncclComm_t comm,
                       hipStream_t st) {
     g_calls[kRecv]++;
+    t_calls[kRecv]++;
     return enqueue(false, buf, count, t, peer, comm, st);
 }
 
 ncclResult_t ncclAllGather(const void *send, void *recv, size_t count, ncclDataType_t t,
                            ncclComm_t comm, hipStream_t st) {
     g_calls[kAllGather]++;
+    t_calls[kAllGather]++;
     return collective(kCollAllGather, send, recv, count, t, 0, comm, st);
 }
 
 ncclResult_t ncclAllReduce(const void *send, void *recv, size_t count, ncclDataType_t t,
                            ncclRedOp_t op, ncclComm_t comm, hipStream_t st) {
     g_calls[kAllReduce]++;
+    t_calls[kAllReduce]++;
     if (op != ncclSum) return bad(ncclInvalidArgument, "all-reduce: only ncclSum is implemented");
     return collective(kCollAllReduce, send, recv, count, t, 0, comm, st);
 }
@@ -530,6 +541,7 @@ ncclResult_t ncclAllReduce(const void *send, void *recv, size_t count, ncclDataT
 ncclResult_t ncclBroadcast(const void *send, void *recv, size_t count, ncclDataType_t t,
                            int root, ncclComm_t comm, hipStream_t st) {
     g_calls[kBroadcast]++;
+    t_calls[kBroadcast]++;
     if (!comm || root < 0 || root >= comm->world)
         return bad(ncclInvalidArgument, "broadcast: bad root");
     return collective(kCollBroadcast, send, recv, count, t, root, comm, st);
@@ -542,6 +554,12 @@ long fake_rccl_calls(const char *name) {
     return -1;
 }
 long fake_rccl_bytes(void) { return g_bytes.load(); }
+// the calls made by the calling thread (one rank) so far
+long fake_rccl_thread_calls(const char *name) {
+    for (int i = 0; i < kNumFn; ++i)
+        if (!strcmp(name, kFnNames[i])) return t_calls[i];
+    return -1;
+}
 const char *fake_rccl_error(void) {
     std::lock_guard<std::mutex> g(g_err_mu);
     return g_err.c_str();

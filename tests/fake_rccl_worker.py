@@ -39,8 +39,8 @@ from hpcclassmultigridproject_amd import (Multigrid, _lib, init_problem,  # noqa
 from hpcclassmultigridproject_amd import dist as D  # noqa: E402
 
 NU = -4e-4
-CALLS = ["ncclCommInitRank", "ncclGroupStart", "ncclGroupEnd", "ncclSend", "ncclRecv",
-         "ncclAllGather", "ncclAllReduce", "ncclBroadcast", "ncclCommDestroy"]
+CALLS = ["ncclCommInitRank", "ncclCommSplit", "ncclGroupStart", "ncclGroupEnd", "ncclSend",
+         "ncclRecv", "ncclAllGather", "ncclAllReduce", "ncclBroadcast", "ncclCommDestroy"]
 
 
 def fake():
@@ -49,24 +49,42 @@ def fake():
     f.fake_rccl_calls.argtypes = [C.c_char_p]
     f.fake_rccl_error.restype = C.c_char_p
     f.fake_rccl_bytes.restype = C.c_long
+    f.fake_rccl_thread_calls.restype = C.c_long
+    f.fake_rccl_thread_calls.argtypes = [C.c_char_p]
     return f
 
 
-def sequence(mg, full_download, upload):
-    """The calls every rank (and the one-GPU context) makes; -> results."""
-    out = {}
+def sequence(mg, full_download, upload, calls=None):
+    """The calls every rank (and the one-GPU context) makes; -> results.
+    Per phase: the cross-pass launches (K_XSMOOTH events of this context) and,
+    when `calls` is given (a rank), the NCCL calls this rank made in it."""
+    out = {"phase_xsmooth": {}, "phase_calls": {}}
     upload(mg)
     mg.profile(True, finest_only=True)
-    mg.rhs()
-    out["norms"] = [mg.run_cycles(1) for _ in range(2)]
+
+    def phase(name, fn):
+        mg.synchronize()
+        c0 = calls() if calls else None
+        mg.profile_reset()
+        r = fn()
+        mg.synchronize()
+        out["phase_xsmooth"][name] = mg.profile_get(_lib.K_XSMOOTH, 0)[0]
+        if calls:
+            c1 = calls()
+            out["phase_calls"][name] = {k: c1[k] - c0[k] for k in c1}
+        return r
+
+    phase("rhs", mg.rhs)
+    out["norms"] = [phase(f"cycle{i}", lambda: mg.run_cycles(1)) for i in range(2)]
     out["u_cycles"] = mg.download_rows(0)
     if full_download:
         out["u_full"] = mg.download()
-    out["steps"] = [mg.step() for _ in range(2)]
+    out["steps"] = [phase(f"step{i}", mg.step) for i in range(2)]
     out["u_steps"] = mg.download_rows(0)
-    mg.mg_inner()   # no norm: the plain partitioned V-cycle on every level
+    # no norm: the plain partitioned V-cycle on every level
+    phase("vcycle", mg.mg_inner)
     out["u_vcycle"] = mg.download_rows(0)
-    out["xsmooth"] = mg.profile_get(_lib.K_XSMOOTH, 0)[0]
+    out["xsmooth"] = sum(out["phase_xsmooth"].values())
     out["rows"] = mg.owned_rows(0)
     return out
 
@@ -77,11 +95,20 @@ def run_scenario(sc, ref_cache):
     dt = 1.0 / N / 10
     _lib.set_tuning("dist_min_rows", sc.get("min_rows", 256))
     _lib.set_tuning("dist_overlap", sc.get("overlap", 0))
+    fp = _lib.FP_FMA if sc.get("fp") == "fma" else _lib.FP_BITWISE
     u0, v1, v2 = init_problem(N)
-    key = (N, L, tower)
+    key = (N, L, tower, fp)
     if key not in ref_cache:
-        with Multigrid(N, L, dt, NU, device=0, tower_mode=tower) as mg:
-            ref_cache[key] = sequence(mg, True, lambda m: m.upload(u0, v1, v2))
+        # (step_cross off: its time-step cross pass is single-GPU only, so with
+        # it the one-GPU context's steps would launch one cross pass more than
+        # the partitioned ones; the results are bitwise the same either way)
+        old_sc = _lib.get_tuning("step_cross")
+        try:
+            _lib.set_tuning("step_cross", 0)
+            with Multigrid(N, L, dt, NU, device=0, tower_mode=tower, fp_mode=fp) as mg:
+                ref_cache[key] = sequence(mg, True, lambda m: m.upload(u0, v1, v2))
+        finally:
+            _lib.set_tuning("step_cross", old_sc)
     ref = ref_cache[key]
     full = sc.get("full_download", False)
     uid = D.unique_id()
@@ -98,8 +125,8 @@ def run_scenario(sc, ref_cache):
                     with upload_lock:
                         m.upload(u0, v1, v2)
             with Multigrid(N, L, dt, NU, device=0, world=G, rank=r, unique_id=uid,
-                           tower_mode=tower) as mg:
-                out = sequence(mg, full, upload)
+                           tower_mode=tower, fp_mode=fp) as mg:
+                out = sequence(mg, full, upload, calls_now)
                 out["la"] = mg.dist_info()[2]
             res[r] = out
         except Exception as e:   # noqa: BLE001 -- reported to the test
@@ -136,13 +163,27 @@ def run_scenario(sc, ref_cache):
         verdict["steps_equal"] = verdict["steps_equal"] and res[r]["steps"] == ref["steps"]
     verdict["cycles_per_step"] = res[0]["steps"]
     verdict["xsmooth_launches"] = [res[r]["xsmooth"] for r in range(G)]
+    verdict["ref_xsmooth_launches"] = ref["xsmooth"]
+    verdict["phase_xsmooth"] = [res[r]["phase_xsmooth"] for r in range(G)]
+    verdict["ref_phase_xsmooth"] = ref["phase_xsmooth"]
+    # NCCL calls per phase of every rank (thread-local counters of the fake)
+    verdict["phase_calls"] = [res[r]["phase_calls"] for r in range(G)]
     verdict["replicated_level"] = res[0]["la"]
     return verdict
 
 
+_FAKE = None
+
+
+def calls_now():
+    """NCCL calls made so far by the calling thread (this rank)."""
+    return {n: _FAKE.fake_rccl_thread_calls(n.encode()) for n in CALLS}
+
+
 def main():
+    global _FAKE
     scenarios = json.loads(open(sys.argv[1]).read())
-    f = fake()
+    f = _FAKE = fake()
     ref_cache = {}
     out = {"scenarios": []}
     for sc in scenarios:

@@ -92,7 +92,6 @@ TUNING_KEYS = {   # key -> (a valid value, an invalid value or None)
     "march_min_rows": (96, 4), "coarse_lds": (0, 2), "step_fuse": (0, 2), "march_seg": (0, 2), "xtile_max_rows": (0, -1),
     "post_predict": (-1, -2), "post_only": (-1, -2), "step_cross": (0, 2),
     "sep_velocity": (0, 2), "zero_rows": (0, 2), "march_tile_rows": (32, -1),
-    "xgroup": (1, 2),
 }
 
 

@@ -242,27 +242,48 @@ def test_one_segment_per_workgroup_plan(N, L, G, cross, knobs):
     np.testing.assert_allclose(n1, n0, rtol=NORM_RTOL)
 
 
-@pytest.mark.parametrize("N,L,cyc", [(8192, 3, 4), (4096, 6, 4)], ids=["split", "tiled"])
-def test_group_exchange_is_bitwise(N, L, cyc):
-    """Tuning key "xgroup": the interior cross pass as groups of four adjacent
-    strips exchanging their edge columns through LDS (k_xsmooth<..., XG>).
-    u, and the norms to 1e-11, equal the separate-strip kernel's after several
-    cycles -- N=8192, L=3 has march segments starting 14 rows below their
-    first aligned step (band starts 584, 3294, 6004), where the round-3 first
-    version leaked warm-up garbage into the restriction; N=4096 runs the XG
-    march beside k_xtile edge tiles."""
-    old = _lib.get_tuning("xgroup")
-    out = {}
+@pytest.mark.parametrize("N,L,kw", [(4096, 4, {}), (4096, 5, dict(nsmooth=2)),
+                                    (8192, 4, dict(fp_mode=_lib.FP_FMA))],
+                         ids=["N4096", "N4096nu2", "N8192fma"])
+def test_wcycle_cross_passes_equal_unfused(N, L, kw, cross):
+    """W-cycles (shape 2, multigrid.cpp:52): the two level-0 visits of a cycle
+    are fused (visit 1's post- with visit 2's pre-smoothing) and the last one
+    with the next cycle's pre-smoothing -- two cross passes per W-cycle, u
+    bitwise the unfused schedule's, norms to 1e-11."""
+    u_ref, n_ref, x_ref = _cycles(N, L, 4, 0, cross, shape=2, **kw)
+    u_x, n_x, x_x = _cycles(N, L, 4, 1, cross, shape=2, **kw)
+    assert x_ref == 0 and x_x == 2 * 4
+    assert np.array_equal(u_x, u_ref)
+    np.testing.assert_allclose(n_x, n_ref, rtol=NORM_RTOL)
+
+
+def test_wcycle_cross_vs_oracle_and_partitioned(oracle_mod, cross):
+    """The fused W-cycle at N=4096 against the CPU checker's mg_inner (bitwise)
+    and on 4 virtual row blocks (bitwise the one-GPU context)."""
+    O = oracle_mod
+    O.set_threads(8)
+    N, L, cyc = 4096, 4, 2
+    dt = 1.0 / N / 10
+    cross(1)
+    u0, v1, v2 = init_problem(N)
+    t = O.Tower(u0, v1, v2, N, L)
+    O.compute_rhs(t.ufine, N, v1, v2, dt, NU, 1.0 / N, rhs=t.rhsfine)
+    for _ in range(cyc):
+        t.mg_inner(dt, NU, shape=2)
+    old = _lib.get_tuning("dist_min_rows")
     try:
-        for xg in (0, 1):
-            _lib.set_tuning("xgroup", xg)
-            u0, v1, v2 = init_problem(N)
-            with Multigrid(N, L, 1.0 / N / 10, NU) as mg:
+        _lib.set_tuning("dist_min_rows", 16)
+        outs = []
+        for parts in (0, 4):
+            with Multigrid(N, L, dt, NU, shape=2, local_parts=parts) as mg:
                 mg.upload(u0, v1, v2)
                 mg.rhs()
-                norms = [mg.run_cycles(1) for _ in range(cyc)]
-                out[xg] = (mg.download(), norms)
+                mg.profile(True, finest_only=True)
+                for _ in range(cyc):
+                    mg.run_cycles(1)
+                assert mg.profile_get(_lib.K_XSMOOTH, 0)[0] == 2 * cyc
+                outs.append(mg.download())
     finally:
-        _lib.set_tuning("xgroup", old)
-    assert np.array_equal(out[0][0], out[1][0])
-    np.testing.assert_allclose(out[1][1], out[0][1], rtol=NORM_RTOL)
+        _lib.set_tuning("dist_min_rows", old)
+    assert np.array_equal(outs[0], t.ufine)
+    assert np.array_equal(outs[1], outs[0])

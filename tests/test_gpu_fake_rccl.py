@@ -45,6 +45,9 @@ def _scenarios():
     sc.append(dict(N=16384, L=9, world=8, overlap=0))
     sc.append(dict(N=16384, L=9, world=8, overlap=1))
     sc.append(dict(N=16384, L=9, world=8, overlap=2))
+    # fp_mode fma: bitwise the one-GPU fma context (partition-independent forms)
+    sc.append(dict(N=4096, L=7, world=4, min_rows=16, overlap=1, fp="fma", full_download=True))
+    sc.append(dict(N=16384, L=9, world=8, overlap=2, fp="fma"))
     return sc
 
 
@@ -79,6 +82,8 @@ def test_rccl_branch_with_thread_peers_bitwise_vs_one_gpu(tmp_path):
     print(r.stdout[-6000:])
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-4000:]
     res = json.loads(out.read_text())
+    if os.environ.get("MGX_TEST_OUT"):   # keep the per-phase counts for inspection
+        shutil.copy(out, os.path.join(os.environ["MGX_TEST_OUT"], "fake_rccl_result.json"))
     assert res["fake_error"] == "", res["fake_error"]
     for v in res["scenarios"]:
         sc = v["scenario"]
@@ -88,12 +93,20 @@ def test_rccl_branch_with_thread_peers_bitwise_vs_one_gpu(tmp_path):
         assert v["steps_equal"], sc
         if sc["N"] >= 4096:   # the cross-cycle pass ran on every rank
             assert min(v["xsmooth_launches"]) > 0, (sc, v["xsmooth_launches"])
+        # the same schedule as one GPU: per phase, every rank launched the
+        # cross pass exactly as often as the one-GPU context
+        for r, ph in enumerate(v["phase_xsmooth"]):
+            assert ph == v["ref_phase_xsmooth"], (sc, r, ph, v["ref_phase_xsmooth"])
         assert v["replicated_level"] >= 2, sc
     # every NCCL call site of dist.hip ran: ghost send/recv in groups, the
     # in-place all-gathers (coarse rhs, download, row upload's velocity level),
     # the norm all-reduce, the download's broadcast
     calls = res["calls"]
     for name in ("ncclSend", "ncclRecv", "ncclGroupStart", "ncclGroupEnd", "ncclAllGather",
-                 "ncclAllReduce", "ncclBroadcast", "ncclCommInitRank", "ncclCommDestroy"):
+                 "ncclAllReduce", "ncclBroadcast", "ncclCommInitRank", "ncclCommSplit",
+                 "ncclCommDestroy"):
         assert calls[name] > 0, (name, calls)
     assert calls["ncclGroupStart"] == calls["ncclGroupEnd"]
+    # every context splits one side-stream communicator off its own
+    assert calls["ncclCommSplit"] == calls["ncclCommInitRank"]
+    assert calls["ncclCommDestroy"] == 2 * calls["ncclCommInitRank"]

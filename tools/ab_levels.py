@@ -13,12 +13,15 @@ ap.add_argument('--rounds', type=int, default=3)
 ap.add_argument('--cycles', type=int, default=5)
 ap.add_argument('--N', type=int, default=16384)
 ap.add_argument('--L', type=int, default=9)
+ap.add_argument('--shape', type=int, default=1, help='1 V-cycle, 2 W-cycle')
+ap.add_argument('--fp', choices=['bitwise', 'fma'], default='bitwise')
 a = ap.parse_args()
 knobs = [(k, [int(x) for x in v.split(',')]) for k, v in (kv.split('=') for kv in a.knobs)]
 N, L = a.N, a.L
 dt = 1.0 / N / 10
 u0, v1, v2 = pkg.init_problem(N, nthreads=16)
-mg = pkg.Multigrid(N, L, dt, -4e-4, device=0)
+mg = pkg.Multigrid(N, L, dt, -4e-4, device=0, shape=a.shape,
+                   fp_mode=_lib.FP_FMA if a.fp == 'fma' else _lib.FP_BITWISE)
 mg.upload(u0, v1, v2); mg.rhs()
 res = {}
 for rnd in range(a.rounds):

@@ -3,21 +3,21 @@
 hbm_read_bytes = 2 x FETCH_SIZE KiB (gfx950 FETCH_SIZE counts half of a
 16-B/lane streaming read, MI355X_MICROARCH.md HBM section); hbm_write_bytes =
 WRITE_SIZE KiB (exact for 16-B/lane streaming stores).  Means per dispatch."""
-import hashlib
 import json
 import os
 import sys
 
-KERNELS_HIP = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
-                           "hpcclassmultigridproject_amd", "csrc", "kernels.hip")
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from bench import kernels_sha  # noqa: E402  (sha256 of the stencil kernel sources)
 
 src = json.load(open(sys.argv[1]))
 out = {"note": "rocprofv3 --pmc, one counter group per run (tools/pmc_collect.sh), "
                "N=16384 L=9, mean per dispatch; hbm_read_bytes = 2 x FETCH_SIZE KiB "
                "(gfx950 FETCH_SIZE counts half of a 16-B/lane streaming read, "
                "MI355X_MICROARCH.md HBM); hbm_write_bytes = WRITE_SIZE KiB",
-       # bench.py uses these bytes only while kernels.hip is unchanged
-       "kernels_hip_sha256": hashlib.sha256(open(KERNELS_HIP, "rb").read()).hexdigest(),
+       # bench.py uses these bytes only while the kernel sources are unchanged
+       "kernel_sources_sha256": kernels_sha(),
+       "mode": os.environ.get("MGX_PMC_MODE", "fma"),
        "kernels": {}}
 for k, v in src.items():
     if "FETCH_SIZE" not in v or "WRITE_SIZE" not in v:

@@ -1,14 +1,21 @@
-"""Per-kernel resource usage of kernels.hip (VGPRs, spills, LDS, occupancy)
-from hipcc's -Rpass-analysis=kernel-resource-usage remarks.
-    python tools/kres.py [filter] [extra -D flags...]"""
+"""Per-kernel resource usage of the stencil kernels (VGPRs, spills, LDS,
+occupancy) from hipcc's -Rpass-analysis=kernel-resource-usage remarks.
+    python tools/kres.py [filter] [extra -D flags...]
+The source file follows the filter: xsmooth / xtile -> xsmooth.hip, wsmooth /
+smooth_tile -> wsmooth.hip, else kernels.hip; MGX_KRES_DIR overrides the
+source directory (e.g. an older checkout)."""
+import os
 import re
 import subprocess
 import sys
 
 flt = sys.argv[1] if len(sys.argv) > 1 else "xsmooth"
+src = ("xsmooth.hip" if ("xsmooth" in flt or "xtile" in flt) else
+       "wsmooth.hip" if ("wsmooth" in flt or "smooth_tile" in flt) else "kernels.hip")
+srcdir = os.environ.get("MGX_KRES_DIR", "hpcclassmultigridproject_amd/csrc")
 cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
        "-ffp-contract=off", "-fno-fast-math", "-Wno-pass-failed", "--cuda-device-only", "-c",
-       "-o", "/tmp/kres.o", "hpcclassmultigridproject_amd/csrc/kernels.hip",
+       "-o", "/tmp/kres.o", os.path.join(srcdir, src),
        "-Rpass-analysis=kernel-resource-usage"] + sys.argv[2:]
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
 cur = None
