@@ -14,6 +14,9 @@
 //
 // Flags (all optional): -N n  -L maxlvl  -nu nu  -steps s  -tol t  -shape 1|2
 //                       -nsmooth k  -tower 0|1  -out prefix  -cuda (also write uTcuda.txt)
+//                       -fp bitwise|fma (run 2's arithmetic, mgx_options.fp_mode;
+//                       fma: the printed error is then the fma path's L1 distance
+//                       from the bitwise one)
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -101,6 +104,7 @@ int main(int argc, char **argv) {
     int maxlvl = -1, shape = 1, nsmooth = 3, steps = -1, tower = MGX_TOWER_REFERENCE;
     double nu = -4 * 1e-4, tol = 1e-6;              // :235, :240
     bool cuda_file = false;
+    int fp_mode = MGX_FP_BITWISE;
     std::string prefix;
     for (int a = 1; a < argc; ++a) {
         std::string k = argv[a];
@@ -121,6 +125,15 @@ int main(int argc, char **argv) {
         else if (k == "-tower") tower = atoi(next());
         else if (k == "-out") prefix = next();
         else if (k == "-cuda") cuda_file = true;
+        else if (k == "-fp") {
+            const std::string v = next();
+            if (v == "fma") fp_mode = MGX_FP_FMA;
+            else if (v == "bitwise") fp_mode = MGX_FP_BITWISE;
+            else {
+                fprintf(stderr, "-fp takes bitwise or fma\n");
+                return 2;
+            }
+        }
         else {
             fprintf(stderr, "unknown flag %s\n", k.c_str());
             return 2;
@@ -149,6 +162,7 @@ int main(int argc, char **argv) {
     o.shape = shape;
     o.nsmooth = nsmooth;
     o.tower_mode = tower;
+    o.fp_mode = fp_mode;
     t0 = std::chrono::steady_clock::now();
     die(mgx_timestepper_ex(uTfast.data(), u0.data(), v1.data(), v2.data(), nu, maxlvl, N, dt, T,
                            dx, tol, &o, nullptr),

@@ -36,10 +36,12 @@
 namespace mgxi {
 
 long g_dist_min_rows = 256;
-// tuning key "dist_overlap": 1 = the finest level's u ghost rows are exchanged
-// on a second stream as soon as the pass that wrote them ends, hidden behind
-// the coarse levels of the V-cycle (the level-0 pass that reads them waits
-// for it); 2 = that, and the cross pass's remaining exchange (level-1 u) on
+// tuning key "dist_overlap": 1 = every partitioned level's u ghost rows are
+// exchanged on a second stream (its own communicator) as soon as the pass
+// that wrote them ends -- the pre-smoothing pass, or the finest level's cross
+// pass -- hidden behind the coarser levels of the V-cycle (the level's post
+// pass waits for it, and then exchanges only the coarser level's u for its
+// prolongation); 2 = that, and the cross pass's remaining exchange (level-1 u) on
 // the second stream too, beside the pass's interior march (the bands next to
 // the ghosts go to its edge launch); 0 = every exchange on the
 // compute stream; -1 (default) = 1 on an RCCL communicator, 0 on virtual
@@ -119,11 +121,16 @@ struct Dist {
     double *hsum = nullptr;    // pinned
     // dist_overlap: ghost exchanges on a second stream beside the interior pass
     hipStream_t xs = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    // dist_overlap: level-0 u buffer whose ghost rows the side stream has
-    // exchanged (or is exchanging: early_pending) since it was last written, or -1
-    int early_buf = -1;
-    bool early_pending = false;
+    hipEvent_t ev_fork = nullptr;
+    hipEvent_t ev_join = nullptr;   // the side stream's last recorded work
+    bool early_pending = false;     // side-stream work the compute stream has not joined
+    // dist_overlap, per partitioned level l: the u buffer whose ghost rows the
+    // side stream has exchanged (or is exchanging) since it was last written,
+    // or -1; ev_lvl[l] marks the end of that exchange, lvl_pending[l] = not yet
+    // waited for by the compute stream
+    std::vector<int> early_buf;
+    std::vector<hipEvent_t> ev_lvl;
+    std::vector<char> lvl_pending;
 };
 
 // the effective dist_overlap of a context (-1: by transport)
@@ -155,6 +162,8 @@ void dist_free(mgx_ctx *c) {
     if (d->xs) (void)hipStreamDestroy(d->xs);
     if (d->ev_fork) (void)hipEventDestroy(d->ev_fork);
     if (d->ev_join) (void)hipEventDestroy(d->ev_join);
+    for (hipEvent_t e : d->ev_lvl)
+        if (e) (void)hipEventDestroy(e);
     if (d->hsum) (void)hipHostFree(d->hsum);
     delete d;
     c->dist = nullptr;
@@ -174,6 +183,10 @@ static int build_dist(mgx_ctx *c, int world, const std::vector<int> &ranks) {
     HIPCHK(hipStreamCreateWithFlags(&d->xs, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&d->ev_join, hipEventDisableTiming));
+    d->early_buf.assign(d->la, -1);
+    d->lvl_pending.assign(d->la, 0);
+    d->ev_lvl.assign(d->la, nullptr);
+    for (auto &e : d->ev_lvl) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (int r : ranks) {
         Part p;
         p.rank = r;
@@ -299,18 +312,22 @@ static int xchg(mgx_ctx *c, const std::vector<XF> &xs) {
 
 static int xchg(mgx_ctx *c, int l, Field f) { return xchg(c, std::vector<XF>{XF{l, f}}); }
 
-// The side stream's work is joined into the compute stream (dist_overlap).
+// All of the side stream's work is joined into the compute stream (dist_overlap).
 static int settle(mgx_ctx *c) {
     Dist *d = c->dist;
     if (!d->early_pending) return MGX_OK;
     HIPCHK(hipStreamWaitEvent(c->stream, d->ev_join, 0));
     d->early_pending = false;
+    std::fill(d->lvl_pending.begin(), d->lvl_pending.end(), 0);
     return MGX_OK;
 }
 
-// Records the side stream's exchange like a launch (launch() times c->stream).
+// Records the side stream's exchange like a launch (launch() times c->stream);
+// ev_join (and ev_extra) mark its end.  Stream order on the side stream: a
+// later wait on ev_join covers every earlier side exchange too.
 template <class F>
-static int side_exchange(mgx_ctx *c, const std::vector<XF> &xs, F &&post) {
+static int side_exchange(mgx_ctx *c, const std::vector<XF> &xs, F &&post,
+                         hipEvent_t ev_extra = nullptr) {
     Dist *d = c->dist;
     HIPCHK(hipEventRecord(d->ev_fork, c->stream));
     HIPCHK(hipStreamWaitEvent(d->xs, d->ev_fork, 0));
@@ -324,30 +341,43 @@ static int side_exchange(mgx_ctx *c, const std::vector<XF> &xs, F &&post) {
         c->pending.push_back({MGX_K_HALO, 0, b, b, e0, e1});
     }
     HIPCHK(hipEventRecord(d->ev_join, d->xs));
+    if (ev_extra) HIPCHK(hipEventRecord(ev_extra, d->xs));
+    d->early_pending = true;
     post();
     return MGX_OK;
 }
 
-// dist_overlap: the level-0 u ghost rows of buffer b (just written, next read
-// by a level-0 pass after the coarse levels) exchanged on the side stream now.
-static int early_u0(mgx_ctx *c, int b) {
+// dist_overlap: the u ghost rows of buffer b of partitioned level l, just
+// written by the level's pre-smoothing pass (or the finest level's cross
+// pass) and next read by the level's post-smoothing pass after the coarser
+// levels, exchanged on the side stream now -- behind the coarse part of the
+// V-cycle instead of in front of the post pass.
+static int early_u(mgx_ctx *c, int l, int b) {
     Dist *d = c->dist;
-    if (overlap_mode(d) == 0 || d->world == 1 || d->la < 1) return MGX_OK;
-    CHK(settle(c));
-    return side_exchange(c, {XF{0, kU, b}}, [&] {
-        d->early_pending = true;
-        d->early_buf = b;
-    });
+    if (overlap_mode(d) == 0 || d->world == 1 || l >= d->la) return MGX_OK;
+    return side_exchange(
+        c, {XF{l, kU, b}},
+        [&] {
+            d->lvl_pending[l] = 1;
+            d->early_buf[l] = b;
+        },
+        d->ev_lvl[l]);
 }
 
-// Whether the current level-0 u buffer's ghost rows are already exchanged
-// (early_u0); joins the side stream.  Consumes the state.
-static int take_fresh(mgx_ctx *c, bool *fresh) {
+// Whether the current u buffer of level l has its ghost rows exchanged
+// already (early_u); the compute stream waits for that exchange.  Consumes
+// the state.
+static int take_fresh(mgx_ctx *c, int l, bool *fresh) {
     Dist *d = c->dist;
-    CHK(settle(c));
-    *fresh = d->early_buf >= 0 && !d->parts.empty() && !d->parts[0].lv.empty() &&
-             d->early_buf == d->parts[0].lv[0].cur;
-    d->early_buf = -1;
+    *fresh = false;
+    if (l >= d->la) return MGX_OK;
+    if (d->lvl_pending[l]) {
+        HIPCHK(hipStreamWaitEvent(c->stream, d->ev_lvl[l], 0));
+        d->lvl_pending[l] = 0;
+    }
+    *fresh = d->early_buf[l] >= 0 && !d->parts.empty() &&
+             d->early_buf[l] == d->parts[0].lv[l].cur;
+    d->early_buf[l] = -1;
     return MGX_OK;
 }
 
@@ -427,8 +457,8 @@ static int smooth(mgx_ctx *c, int l, bool prolong, bool restrict_, bool norm) {
     Dist *d = c->dist;
     const int sweeps = c->opt.nsmooth;
     const int fuse = std::max(1, std::min(c->opt.fuse, mgx::kSmoothMaxSweeps));
-    bool fresh = false;   // level 0: u ghosts exchanged early (dist_overlap)
-    if (l == 0) CHK(take_fresh(c, &fresh));
+    bool fresh = false;   // u ghosts exchanged early (dist_overlap)
+    CHK(take_fresh(c, l, &fresh));
     for (int done = 0; done < sweeps;) {
         const int k = std::min(sweeps - done, fuse);
         const bool first = done == 0, last = done + k == sweeps;
@@ -505,6 +535,7 @@ static int dist_level(mgx_ctx *c, int l, bool want_norm) {
         const bool last = sh == c->opt.shape - 1;
         CHK(smooth(c, l, false, /*restrict=*/true, false));
         CHK(coarse_rhs_ready(c, l));
+        CHK(early_u(c, l, c->dist->parts[0].lv[l].cur));
         CHK(coarse_cycle(c, l + 1));
         CHK(smooth(c, l, /*prolong=*/true, false, want_norm && last));
     }
@@ -537,7 +568,7 @@ static void dist_drop_spec(mgx_ctx *c) {
 // is made ready on level 1 and the per-rank norm sums are reduced by the caller.
 //
 // dist_overlap >= 1: the level-0 ghosts were exchanged on the side stream
-// right after the pass that wrote them (early_u0), behind the coarse levels;
+// right after the pass that wrote them (early_u), behind the coarse levels;
 // only level 1's u ghosts remain.  dist_overlap = 2: those go on the second
 // stream too (forked after the work that produced the sent rows) while the
 // compute stream runs the pass's unguarded interior march over rows
@@ -552,7 +583,7 @@ static int dist_cross(mgx_ctx *c, bool store_post) {
     const int k = c->opt.nsmooth;
     // u ghosts of level 0 (unless exchanged early, dist_overlap) and of level 1
     bool fresh = false;
-    CHK(take_fresh(c, &fresh));
+    CHK(take_fresh(c, 0, &fresh));
     std::vector<XF> xl;
     if (!fresh) xl.push_back(XF{0, kU});
     if (1 < d->la) xl.push_back(XF{1, kU});
@@ -667,7 +698,7 @@ static int dist_cross(mgx_ctx *c, bool store_post) {
     // the next cycle's level-0 input is u_pre: its ghosts now, on the side
     // stream, behind the coarse levels (after the coarse rhs exchange, which
     // the next level needs first)
-    return early_u0(c, d->parts[0].lv[0].spec);
+    return early_u(c, 0, d->parts[0].lv[0].spec);
 }
 
 bool dist_post_predictable(mgx_ctx *c) {
@@ -711,7 +742,7 @@ int dist_vcycle(mgx_ctx *c, double *norm, bool store_post) {
         } else {
             CHK(smooth(c, 0, false, /*restrict=*/true, false));
             CHK(coarse_rhs_ready(c, 0));
-            CHK(early_u0(c, d->parts[0].lv[0].cur));
+            CHK(early_u(c, 0, d->parts[0].lv[0].cur));
         }
         // W-cycles: visit sh's post- and visit sh+1's pre-smoothing as one
         // cross pass (mgx.hip:op_vcycle)
@@ -844,7 +875,7 @@ int dist_upload(mgx_ctx *c, const double *u0, const double *v1, const double *v2
     Dist *d = c->dist;
     HIPCHK(hipSetDevice(c->device));
     CHK(settle(c));
-    d->early_buf = -1;
+    std::fill(d->early_buf.begin(), d->early_buf.end(), -1);
     mgx_options o = c->opt;
     o.device = -1;
     mgx_ctx *T = nullptr;
@@ -1003,7 +1034,7 @@ static int dist_upload_rows_impl(mgx_ctx *c, const double *const *u0s,
     Dist *d = c->dist;
     HIPCHK(hipSetDevice(c->device));
     CHK(settle(c));
-    d->early_buf = -1;
+    std::fill(d->early_buf.begin(), d->early_buf.end(), -1);
     if (c->opt.tower_mode != MGX_TOWER_CORRECT)
         return fail(MGX_E_ARG, "mgx_upload_rows: needs tower_mode MGX_TOWER_CORRECT (the "
                                "reference tower mixes rows of the whole grid)");

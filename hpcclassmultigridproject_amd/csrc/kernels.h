@@ -18,8 +18,8 @@ struct Coef {
     double rr, nu, h, dgs, drhs, rdgs;   // rdgs = RN(1/dgs)
     unsigned dsign;                       // sign bit of dgs (high-word position)
     // fp_mode fma (MGX_FP_FMA): the operator divided by its diagonal, see
-    // stencil.h "fp_mode fma".  g = rr/d, gn = g*nu.
-    double g, gn;
+    // stencil.h "fp_mode fma".  g = rr/d, gn = g*nu, c2 = -2 gn.
+    double g, gn, c2;
     int fm;   // 1: the smoothing passes run the contracted (fma) forms
 };
 // fm: the context's fp_mode (0 bitwise, 1 fma)

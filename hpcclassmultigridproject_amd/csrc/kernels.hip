@@ -28,6 +28,7 @@ Coef make_coef(double k, double nu, double h, int fm) {
     c.dsign = std::signbit(c.dgs) ? 0x80000000u : 0u;
     c.g = c.rr / c.dgs;
     c.gn = c.g * nu;
+    c.c2 = -2.0 * c.gn;
     c.fm = fm ? 1 : 0;
     return c;
 }

@@ -360,23 +360,26 @@ __device__ __forceinline__ double rhs_point_t(double t1, double t2, double u, do
 // ---------------------------------------------------------------- fp_mode fma
 // MGX_FP_FMA (Coef::fm): the smoothing passes evaluate gs.cpp:126-130 divided
 // by the diagonal d and contracted,
-//   u = f' + mn*uN + mw*uW + me*uE + ms*uS,   f' = f/d,  m = -(coefficient)/d:
-//   mn = g*t1 - gn, ms = -g*t1 - gn (from v1: cc, dd), mw = g*t2 - gn,
-//   me = -g*t2 - gn (from v2: aa, bb), with t = v*h/2, g = rr/d, gn = g*nu --
+//   u = f' + mn*uN + mw*uW + me*uE + ms*uS,   f' = f/d,  m = -(coefficient)/d,
+// with t = v*h/2, g = rr/d, gn = g*nu:
+//   mn = g*t1 - gn, mw = g*t2 - gn   (-cc/d from v1, -aa/d from v2), one fma;
+//   ms = c2 - mn,   me = c2 - mw     (-dd/d, -bb/d: cc + dd = aa + bb = 2 rr nu,
+//                                     c2 = -2 gn), one subtraction --
 // four v_fma_f64 per update against 4 mul + 4 sub + the 3-op division of the
-// bitwise form (gs.cpp:130 evaluated term by term), and one fma per
-// coefficient instead of a sub and a mul.  The residual (gs.cpp:75) is
-// d*(GS update - u).  Not bitwise the reference: each value within a few
+// bitwise form (gs.cpp:130 evaluated term by term).  The residual (gs.cpp:75)
+// is d*(GS update - u).  Not bitwise the reference: each value within a few
 // ulp (max|duT| <= 1e-12, the same cycle counts).  The freshest
 // neighbour (uS, written by the previous stage of the same step) enters last.
 // Every kernel (row marches, LDS tiles, coarsest solve) forms the same values
-// from t = fl(v*h/2) with the same operations, so fma-mode results do not
-// depend on which kernel, tile size or row partition computed a point.
+// from t = fl(v*h/2) with the same operations -- a kernel may keep ms / me per
+// row or recompute them per update (fewer registers), the bits are the same --
+// so fma-mode results do not depend on which kernel, tile size or row
+// partition computed a point.
 __device__ __forceinline__ double fm_mp(double t, const Coef &c) {   // mn / mw
     return __builtin_fma(c.g, t, -c.gn);
 }
-__device__ __forceinline__ double fm_mm(double t, const Coef &c) {   // ms / me
-    return __builtin_fma(-c.g, t, -c.gn);
+__device__ __forceinline__ double fm_ms(double m, const Coef &c) {   // ms / me from mn / mw
+    return c.c2 - m;
 }
 __device__ __forceinline__ double fm_upd(double fs, double mn, double uN, double mw, double uW,
                                          double ms, double uS, double me, double uE) {
@@ -388,15 +391,23 @@ __device__ __forceinline__ double fm_res(double fs, double u, double mn, double 
                                          const Coef &c) {
     return (fm_upd(fs, mn, uN, mw, uW, ms, uS, me, uE) - u) * c.dgs;
 }
+// from mn, mw only (ms, me recomputed)
+__device__ __forceinline__ double fm_upd2(double fs, double mn, double uN, double mw, double uW,
+                                          double uS, double uE, const Coef &c) {
+    return fm_upd(fs, mn, uN, mw, uW, fm_ms(mn, c), uS, fm_ms(mw, c), uE);
+}
+__device__ __forceinline__ double fm_res2(double fs, double u, double mn, double uN, double mw,
+                                          double uW, double uS, double uE, const Coef &c) {
+    return fm_res(fs, u, mn, uN, mw, uW, fm_ms(mn, c), uS, fm_ms(mw, c), uE, c);
+}
 // from t1, t2 (no stored coefficients)
 __device__ __forceinline__ double fm_upd_t(double fs, double t1, double t2, double uN, double uW,
                                            double uS, double uE, const Coef &c) {
-    return fm_upd(fs, fm_mp(t1, c), uN, fm_mp(t2, c), uW, fm_mm(t1, c), uS, fm_mm(t2, c), uE);
+    return fm_upd2(fs, fm_mp(t1, c), uN, fm_mp(t2, c), uW, uS, uE, c);
 }
 __device__ __forceinline__ double fm_res_t(double fs, double t1, double t2, double u, double uN,
                                            double uW, double uS, double uE, const Coef &c) {
-    return fm_res(fs, u, fm_mp(t1, c), uN, fm_mp(t2, c), uW, fm_mm(t1, c), uS, fm_mm(t2, c), uE,
-                  c);
+    return fm_res2(fs, u, fm_mp(t1, c), uN, fm_mp(t2, c), uW, uS, uE, c);
 }
 
 inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }

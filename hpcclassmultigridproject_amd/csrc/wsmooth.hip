@@ -65,6 +65,11 @@ struct WCfg {
     // rows an unguarded march may own: its warm-up updates rows down to
     // E + NR + S - 2 above the first, its drain E - 2 below the last
     static constexpr int TOP = E + NR + S + 2, BOT = E + 4;
+#ifndef MGX_WMINB
+#define MGX_WMINB 1
+#endif
+    // workgroups per CU the compiler must fit (launch bounds)
+    static constexpr int MINB = MGX_WMINB;
 };
 
 // rhs/v prefetch distance of the wave march: with t = v*h/2 formed at the
@@ -83,11 +88,12 @@ struct WCfg {
 // (as in k_xsmooth) needs ~110 more VGPRs -- one wave per SIMD, measured
 // slower.  (RHSN: every coefficient per stage.)
 // FM: fp_mode fma (stencil.h): f' = f/d enters the ring at the row's first
-// use, the stored pair is mn, ms, the stages contract (four fmas), residuals
+// use, the stored pair is mn, mw (ms, me recomputed: one subtraction each),
+// the stages contract (four fmas), residuals
 // are d*(update - u); RHSN's rhs keeps the reference expressions (gs.cpp:44,
 // stored unscaled) and is scaled after.
 template <int WPB, int K, int MODE, bool G, bool PD = false, bool FM = false>
-__global__ __launch_bounds__(64 * WPB) void k_wsmooth(
+__global__ __launch_bounds__(64 * WPB, (WCfg<K, MODE>::MINB)) void k_wsmooth(
     const double *__restrict__ uin, double *__restrict__ uout, const double *__restrict__ rhs,
     const double *__restrict__ v1, const double *__restrict__ v2, const double *__restrict__ uc,
     long pitchc, double *__restrict__ rhsc, double *__restrict__ partials, int n, long pitch,
@@ -219,20 +225,20 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
         // from its stored cn, cs (FM: mn, ms)
         auto res_cx = [&](const int iR, const int iN, const int iS, const double uW) {
             const CoefRow &k = cf[iR];
+            if (FM)   // (stored: mn in cn, mw in cw)
+                return fm_res2(rd[iR].r.x, ur[iR].x, k.cn.x, ur[iN].x, k.cw.x, uW, ur[iS].x,
+                               ur[iR].y, c);
             const double t2 = rd[iR].y.x;
-            if (FM)
-                return fm_res(rd[iR].r.x, ur[iR].x, k.cn.x, ur[iN].x, fm_mp(t2, c), uW, k.cs.x,
-                              ur[iS].x, fm_mm(t2, c), ur[iR].y, c);
             const double cw = c.rr * (c.nu - t2), ce = c.rr * (t2 + c.nu);
             return rd[iR].r.x - (c.dgs * ur[iR].x + k.cn.x * ur[iN].x + cw * uW +
                                  k.cs.x * ur[iS].x + ce * ur[iR].y);
         };
         auto res_cy = [&](const int iR, const int iN, const int iS, const double uE) {
             const CoefRow &k = cf[iR];
-            const double t2 = rd[iR].y.y;
             if (FM)
-                return fm_res(rd[iR].r.y, ur[iR].y, k.cn.y, ur[iN].y, fm_mp(t2, c), ur[iR].x,
-                              k.cs.y, ur[iS].y, fm_mm(t2, c), uE, c);
+                return fm_res2(rd[iR].r.y, ur[iR].y, k.cn.y, ur[iN].y, k.cw.y, ur[iR].x,
+                               ur[iS].y, uE, c);
+            const double t2 = rd[iR].y.y;
             const double cw = c.rr * (c.nu - t2), ce = c.rr * (t2 + c.nu);
             return rd[iR].r.y - (c.dgs * ur[iR].y + k.cn.y * ur[iN].y + cw * ur[iR].x +
                                  k.cs.y * ur[iS].y + ce * uE);
@@ -301,9 +307,9 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                 if (WH) {   // cn, cs of row s+1 from t1 (gs.cpp:128-129's cc, dd)
                     const RowData &d1 = rd[(p + 1) % NR];
                     CoefRow &k1 = cf[(p + 1) % NR];
-                    if (FM) {
+                    if (FM) {   // mn, mw (ms, me recomputed per stage: 8 VGPRs per row fewer)
                         k1.cn = make_double2(fm_mp(d1.x.x, c), fm_mp(d1.x.y, c));
-                        k1.cs = make_double2(fm_mm(d1.x.x, c), fm_mm(d1.x.y, c));
+                        k1.cw = make_double2(fm_mp(d1.y.x, c), fm_mp(d1.y.y, c));
                     } else {
                         k1.cn = make_double2(c.rr * (c.nu - d1.x.x), c.rr * (c.nu - d1.x.y));
                         k1.cs = make_double2(c.rr * (d1.x.x + c.nu), c.rr * (d1.x.y + c.nu));
@@ -331,8 +337,8 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                         const double uW = dpp_shr1(ur[iR].y);   // column c0-1
                         if (!G || (inr && in0)) {
                             if (FM && WH)
-                                ur[iR].x = fm_upd(d.r.x, k.cn.x, ur[iN].x, fm_mp(d.y.x, cg), uW,
-                                                  k.cs.x, ur[iS].x, fm_mm(d.y.x, cg), ur[iR].y);
+                                ur[iR].x = fm_upd2(d.r.x, k.cn.x, ur[iN].x, k.cw.x, uW, ur[iS].x,
+                                                   ur[iR].y, cg);
                             else if (FM)
                                 ur[iR].x = fm_upd_t(d.r.x, d.x.x, d.y.x, ur[iN].x, uW, ur[iS].x,
                                                     ur[iR].y, cg);
@@ -350,9 +356,8 @@ __global__ __launch_bounds__(64 * WPB) void k_wsmooth(
                         const double uE = dpp_shl1(ur[iR].x);   // column c0+2
                         if (!G || (inr && in1)) {
                             if (FM && WH)
-                                ur[iR].y = fm_upd(d.r.y, k.cn.y, ur[iN].y, fm_mp(d.y.y, cg),
-                                                  ur[iR].x, k.cs.y, ur[iS].y, fm_mm(d.y.y, cg),
-                                                  uE);
+                                ur[iR].y = fm_upd2(d.r.y, k.cn.y, ur[iN].y, k.cw.y, ur[iR].x,
+                                                   ur[iS].y, uE, cg);
                             else if (FM)
                                 ur[iR].y = fm_upd_t(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x,
                                                     ur[iS].y, uE, cg);

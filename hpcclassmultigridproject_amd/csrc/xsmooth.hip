@@ -318,8 +318,8 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             if (FM) {
                 k.cn = make_double2(fm_mp(d.x.x, c), fm_mp(d.x.y, c));
                 k.cw = make_double2(fm_mp(d.y.x, c), fm_mp(d.y.y, c));
-                k.cs = make_double2(fm_mm(d.x.x, c), fm_mm(d.x.y, c));
-                k.ce = make_double2(fm_mm(d.y.x, c), fm_mm(d.y.y, c));
+                k.cs = make_double2(fm_ms(k.cn.x, c), fm_ms(k.cn.y, c));
+                k.ce = make_double2(fm_ms(k.cw.x, c), fm_ms(k.cw.y, c));
                 return;
             }
             k.cn = make_double2(c.rr * (c.nu - d.x.x), c.rr * (c.nu - d.x.y));
@@ -683,16 +683,16 @@ __global__ __launch_bounds__(256) void k_xtile(
             const double2 rr = ld2(rhs + o), xx = ld2(v1 + o), yy = ld2(v2 + o);
             // gs.cpp:126-129: aa, bb from v2 (W / E), cc, dd from v1 (N / S)
             const double hh = c.h * 0.5;   // FM: from t = v*h/2 (stencil.h)
-            const PtCoef X =
-                FM ? PtCoef{rr.x * c.rdgs, fm_mp(xx.x * hh, c), fm_mp(yy.x * hh, c),
-                            fm_mm(xx.x * hh, c), fm_mm(yy.x * hh, c)}
-                   : PtCoef{rr.x, coef_a(xx.x, c), coef_a(yy.x, c), coef_b(xx.x, c),
-                            coef_b(yy.x, c)};
-            const PtCoef Y =
-                FM ? PtCoef{rr.y * c.rdgs, fm_mp(xx.y * hh, c), fm_mp(yy.y * hh, c),
-                            fm_mm(xx.y * hh, c), fm_mm(yy.y * hh, c)}
-                   : PtCoef{rr.y, coef_a(xx.y, c), coef_a(yy.y, c), coef_b(xx.y, c),
-                            coef_b(yy.y, c)};
+            auto fmc = [&](double f, double t1, double t2) {
+                const double mn = fm_mp(t1, c), mw = fm_mp(t2, c);
+                return PtCoef{f * c.rdgs, mn, mw, fm_ms(mn, c), fm_ms(mw, c)};
+            };
+            const PtCoef X = FM ? fmc(rr.x, xx.x * hh, yy.x * hh)
+                                : PtCoef{rr.x, coef_a(xx.x, c), coef_a(yy.x, c), coef_b(xx.x, c),
+                                         coef_b(yy.x, c)};
+            const PtCoef Y = FM ? fmc(rr.y, xx.y * hh, yy.y * hh)
+                                : PtCoef{rr.y, coef_a(xx.y, c), coef_a(yy.y, c), coef_b(xx.y, c),
+                                         coef_b(yy.y, c)};
             P0[m] = par ? Y : X;
             P1[m] = par ? X : Y;
 #pragma unroll

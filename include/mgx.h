@@ -185,10 +185,11 @@ int mgx_synchronize(mgx_ctx *ctx);
  * the next cycle's restricted rhs, not the last correction.  0 = off.
  * "dist_min_rows": partitioned solvers replicate every level whose row blocks
  * would be shorter than this (default 256, even, >= 16); read at creation.
- * "dist_overlap": partitioned contexts, 1 = the finest level's u
- * ghost rows are exchanged on a second stream as soon as the pass that wrote
- * them ends, hidden behind the coarse levels (the next finest pass waits for
- * it); 2 = that, and the cross pass's remaining exchange (level-1 u) on the
+ * "dist_overlap": partitioned contexts, 1 = every partitioned level's u
+ * ghost rows are exchanged on a second stream (and communicator) as soon as
+ * the pass that wrote them ends, hidden behind the coarser levels (the
+ * level's next pass waits for it); 2 = that, and the cross pass's remaining
+ * exchange (level-1 u) on the
  * second stream beside the pass's interior march, the two 16-row bands next
  * to the ghosts after it; 0 = every exchange on the compute stream; -1
  * (default) = 1 on an RCCL communicator, 0 on virtual ranks (one GPU, where

@@ -46,6 +46,18 @@ def test_multigrid_driver_writes_reference_uT(tmp_path):
     assert "Error (compared to the referenced solution) = 0.000000e+00" in lines
 
 
+def test_multigrid_driver_fma_mode(tmp_path):
+    """./multigrid -fp fma: run 2 (the library's time stepper) contracted; its
+    L1 distance from run 1 (the bitwise op-level sequence) over the N=128
+    grid stays within (N+1)^2 x 1e-12 and is not zero."""
+    exe = _built("multigrid")
+    out = subprocess.run([exe, "-N", "128", "-fp", "fma", "-out", str(tmp_path) + "/"],
+                         capture_output=True, text=True, timeout=300, check=True).stdout
+    m = re.search(r"Error \(compared to the referenced solution\) = (\S+)", out)
+    err = float(m.group(1))
+    assert 0.0 < err <= 129 * 129 * 1e-12, out
+
+
 def test_mg_sweep_formats(tmp_path):
     exe = _built("mg_sweep")
     out = subprocess.run([exe, "-Nmin", "32", "-Nmax", "256", "-cycles", "2", "-steps", "5",

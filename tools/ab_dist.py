@@ -4,7 +4,8 @@ The virtual ranks run one after another on one stream, so G parts ~ 1 GPU's
 work + the partition overheads (ghost rows recomputed, exchanges, more
 launches, replicated coarse levels G times).
     python tools/ab_dist.py [--N 16384 --L 9] [--parts 1,2,4,8] [--cycles 5] [--tower correct]
-                            [--knob key=v1,v2]   (a process-wide tuning key to compare)"""
+                            [--knob key=v1,v2]   (a process-wide tuning key to compare)
+                            [--fp fma|bitwise]   (mgx_options.fp_mode, default fma)"""
 import argparse, json, sys, time
 sys.path.insert(0, '.')
 import hpcclassmultigridproject_amd as pkg
@@ -18,6 +19,7 @@ ap.add_argument('--rounds', type=int, default=2)
 ap.add_argument('--min-rows', default='256')
 ap.add_argument('--overlap', default='0', help='dist_overlap values to compare, e.g. 0,1')
 ap.add_argument('--knob', default=None, help='key=v1,v2: a tuning key to compare')
+ap.add_argument('--fp', choices=['bitwise', 'fma'], default='fma')
 ap.add_argument('--tower', choices=['reference', 'correct'], default='reference',
                 help='correct: no whole-grid staging buffers (N=65536 on one GPU)')
 a = ap.parse_args()
@@ -38,6 +40,7 @@ for rnd in range(a.rounds):
         if G == 1 and ov:
             continue
         mg = pkg.Multigrid(N, L, dt, -4e-4, device=0, local_parts=G if G > 1 else 0,
+                           fp_mode=_lib.FP_FMA if a.fp == 'fma' else _lib.FP_BITWISE,
                            tower_mode=_lib.TOWER_CORRECT if a.tower == 'correct'
                            else _lib.TOWER_REFERENCE)
         if G > 1 and a.tower == 'correct':   # row-block upload (no whole-grid staging)
