@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <initializer_list>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -135,6 +136,7 @@ struct Dist {
 
 // the effective dist_overlap of a context (-1: by transport)
 static long overlap_mode(const Dist *d) {
+    if (d->comm && !d->comm_x) return 0;   // no side-stream communicator
     if (g_dist_overlap >= 0) return g_dist_overlap;
     return d->comm ? 1 : 0;
 }
@@ -1252,11 +1254,14 @@ int mgx_create_dist(mgx_ctx **out, long n, int maxlvl, double dt, double nu,
             free_ctx(c);
             return fail(MGX_E_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
         }
-        // the side stream's communicator (collective: every rank splits here)
+        // the side stream's communicator (collective: every rank splits here);
+        // without it (a split that fails on every rank alike) the context runs
+        // every exchange on the compute stream (overlap_mode 0)
         r = ncclCommSplit(c->dist->comm, 0, rank, &c->dist->comm_x, nullptr);
         if (r != ncclSuccess) {
-            free_ctx(c);
-            return fail(MGX_E_RCCL, std::string("ncclCommSplit: ") + ncclGetErrorString(r));
+            c->dist->comm_x = nullptr;
+            fprintf(stderr, "mgx: ncclCommSplit failed (%s): every exchange stays on the "
+                            "compute stream\n", ncclGetErrorString(r));
         }
     }
     int rc = build_dist(c, world, {rank});

@@ -28,6 +28,37 @@ static int g_threads = 1;
 
 void or_set_threads(int nthreads) { g_threads = nthreads < 1 ? 1 : nthreads; }
 
+/* fp_mode fma (libmgx stencil.h): 0 = the reference's expressions */
+static int g_fm = 0;
+void or_set_fp_mode(int fm) { g_fm = fm ? 1 : 0; }
+
+/* The fma form's constants, as libmgx's make_coef computes them on the host
+ * (kernels.hip): d = 1-4 rr nu, rd = 1/d, g = rr/d, gn = g nu, c2 = -2 gn. */
+typedef struct {
+    double dgs, rdgs, g, gn, c2, hh;
+} FmCoef;
+static FmCoef fm_coef(double k, double nu, double h) {
+    FmCoef f;
+    const double rr = 0.5 * k / (h * h);
+    f.dgs = 1.0 - 4.0 * rr * nu;
+    f.rdgs = 1.0 / f.dgs;
+    f.g = rr / f.dgs;
+    f.gn = f.g * nu;
+    f.c2 = -2.0 * f.gn;
+    f.hh = h * 0.5;
+    return f;
+}
+/* u = f/d + mn uN + mw uW + me uE + ms uS as libmgx evaluates it: t = v*h/2,
+ * mn = fma(g, t1, -gn), mw = fma(g, t2, -gn), ms = c2 - mn, me = c2 - mw,
+ * the fmas in the order N, W, E, S */
+static inline double fm_update(const FmCoef *f, double rhs, double v1, double v2, double uN,
+                               double uW, double uS, double uE) {
+    const double fs = rhs * f->rdgs;
+    const double mn = fma(f->g, v1 * f->hh, -f->gn), mw = fma(f->g, v2 * f->hh, -f->gn);
+    const double ms = f->c2 - mn, me = f->c2 - mw;
+    return fma(ms, uS, fma(me, uE, fma(mw, uW, fma(mn, uN, fs))));
+}
+
 /* gs.cpp:9-11 */
 static inline double coef_r(double h, double k) { return 0.5 * k / (h * h); }
 /* gs.cpp:14-16 */
@@ -63,6 +94,17 @@ void or_residual(double *res, const double *u, const double *rhs, long n,
                  const double *v1, const double *v2, double k, double nu, double h) {
     const double rr = coef_r(h, k);
     const long w = n + 1;
+    if (g_fm) { /* libmgx fp_mode fma: d*(update - u) */
+        const FmCoef f = fm_coef(k, nu, h);
+#pragma omp parallel for schedule(static) if (g_threads > 1) num_threads(g_threads)
+        for (long i = 1; i < n; i++)
+            for (long j = 1; j < n; j++) {
+                const long p = i * w + j;
+                res[p] = (fm_update(&f, rhs[p], v1[p], v2[p], u[p - w], u[p - 1], u[p + w],
+                                    u[p + 1]) - u[p]) * f.dgs;
+            }
+        return;
+    }
 #pragma omp parallel for schedule(static) if (g_threads > 1) num_threads(g_threads)
     for (long i = 1; i < n; i++) {
         for (long j = 1; j < n; j++) {
@@ -92,6 +134,19 @@ static void gs_colour(double *u, const double *rhs, long n, const double *v1,
                       const double *v2, double k, double nu, double h, int colour) {
     const double rr = coef_r(h, k);
     const long w = n + 1;
+    if (g_fm) { /* libmgx fp_mode fma */
+        const FmCoef f = fm_coef(k, nu, h);
+#pragma omp parallel for schedule(static) if (g_threads > 1) num_threads(g_threads)
+        for (long i = 1; i < n; i++) {
+            const long j0 = (colour == 0) ? (2 - (i & 1)) : (1 + (i & 1));
+            for (long j = j0; j < n; j += 2) {
+                const long p = i * w + j;
+                u[p] = fm_update(&f, rhs[p], v1[p], v2[p], u[p - w], u[p - 1], u[p + w],
+                                 u[p + 1]);
+            }
+        }
+        return;
+    }
 #pragma omp parallel for schedule(static) if (g_threads > 1) num_threads(g_threads)
     for (long i = 1; i < n; i++) {
         /* red: odd rows start at j=1, even rows at j=2; black the opposite */
@@ -192,7 +247,10 @@ int or_mg_outer(double **utow, double **v1tow, double **v2tow, double **rhstow,
                 double tol, int shape, int nsmooth, double *res0_out,
                 double *res_out) {
     const int max_cycle = 50; /* multigrid.cpp:94 */
+    const int fm = g_fm; /* (libmgx's initial norm is the reference's residual) */
+    g_fm = 0;
     or_residual(tmp, utow[0], rhstow[0], n, v1tow[0], v2tow[0], dt, nu, dx);
+    g_fm = fm;
     double res0 = or_compute_norm(tmp, n), res = res0;
     int iter;
     for (iter = 0; iter < max_cycle && res / res0 > tol; iter++) {

@@ -85,6 +85,13 @@ void or_init_problem(double *u0, double *v1, double *v2, long N);
 
 /* OpenMP thread count used by the op loops (1 = serial, the default). */
 void or_set_threads(int nthreads);
+/* 1: gauss_seidel and residual in libmgx's fp_mode fma form (stencil.h "fp_mode
+ * fma": the operator divided by its diagonal, four fused multiply-adds per
+ * update, residual d*(update - u)) -- a restatement of the product's
+ * contracted arithmetic, so the GPU fma mode can be checked bit for bit; 0
+ * (default): the reference's term order.  mg_outer's initial norm and
+ * compute_rhs stay the reference's in both (as in libmgx). */
+void or_set_fp_mode(int fm);
 
 #ifdef __cplusplus
 }

@@ -82,6 +82,12 @@ def set_threads(n: int):
     lib().or_set_threads(C.c_int(n))
 
 
+def set_fp_mode(fm: int):
+    """1: the checker's gauss_seidel / residual in libmgx's fp_mode fma form
+    (mg_oracle.h or_set_fp_mode); 0: the reference's term order."""
+    lib().or_set_fp_mode(C.c_int(1 if fm else 0))
+
+
 def compute_rhs(u, n, v1, v2, k, nu, h, rhs=None):
     rhs = np.zeros_like(u) if rhs is None else rhs
     lib().or_compute_rhs(_p(rhs), _p(u), LNG(n), _p(v1), _p(v2), D(k), D(nu), D(h))

@@ -147,3 +147,72 @@ def test_fma_tiles_equal_marches(tile_max_n):
 def test_fma_mode_rejected_value():
     with pytest.raises(_lib.MGXError):
         Multigrid(64, 2, 1e-3, NU, fp_mode=7)
+
+
+# ---- bit for bit against the CPU checker's restatement of the fma form
+# (oracle/mg_oracle.c or_set_fp_mode: the same operations per point), so the
+# fma kernels are pinned to their stated formula, not only to a tolerance
+
+
+@pytest.fixture
+def fm_oracle(oracle_mod):
+    O = oracle_mod
+    O.set_threads(8)
+    O.set_fp_mode(1)
+    yield O
+    O.set_fp_mode(0)
+    O.set_threads(1)
+
+
+@pytest.mark.parametrize("N,L,kw", [(256, 4, {}), (1024, 5, {}), (4096, 3, {}),
+                                    (4096, 4, dict(nsmooth=2)), (2048, 5, dict(shape=2))],
+                         ids=["N256_tiles", "N1024", "N4096_cross", "N4096_nu2", "N2048_W"])
+def test_fma_cycles_bitwise_vs_fma_checker(fm_oracle, N, L, kw):
+    """run_cycles (the cross pass on n >= 4096, wave marches, LDS tiles, the
+    coarsest solve) in fma mode equals the checker's fma mg_inner bit for bit."""
+    O = fm_oracle
+    dt = 1.0 / N / 10
+    nsmooth, shape = kw.get("nsmooth", 3), kw.get("shape", 1)
+    u0, v1, v2 = init_problem(N)
+    t = O.Tower(u0, v1, v2, N, L)
+    O.compute_rhs(t.ufine, N, v1, v2, dt, NU, 1.0 / N, rhs=t.rhsfine)
+    for _ in range(2):
+        t.mg_inner(dt, NU, shape=shape, nsmooth=nsmooth)
+    with Multigrid(N, L, dt, NU, fp_mode=_lib.FP_FMA, **kw) as mg:
+        mg.upload(u0, v1, v2)
+        mg.rhs()
+        mg.run_cycles(2)
+        assert np.array_equal(mg.download(), t.ufine)
+
+
+@pytest.mark.parametrize("N,L,nsmooth,shape", [(512, 4, 3, 2), (4096, 3, 2, 1), (256, 7, 1, 1)])
+def test_fma_mg_outer_bitwise_vs_fma_checker(fm_oracle, N, L, nsmooth, shape):
+    O = fm_oracle
+    dt = 1.0 / N / 10
+    u0, v1, v2 = init_problem(N)
+    t = O.Tower(u0, v1, v2, N, L)
+    O.compute_rhs(t.ufine, N, v1, v2, dt, NU, 1.0 / N, rhs=t.rhsfine)
+    cyc_ref, r0_ref, r_ref = t.mg_outer(dt, NU, 1e-6, shape, nsmooth)
+    with Multigrid(N, L, dt, NU, nsmooth=nsmooth, shape=shape, fp_mode=_lib.FP_FMA) as mg:
+        mg.upload(u0, v1, v2)
+        mg.rhs()
+        cyc, r0, r, _ = mg.mg_outer(1e-6)
+        assert cyc == cyc_ref
+        assert abs(r0 - r0_ref) <= 1e-11 * r0_ref
+        assert abs(r - r_ref) <= 1e-11 * r_ref + norm_floor(N)
+        assert np.array_equal(mg.download(), t.ufine)
+
+
+def test_fma_timestepper_bitwise_vs_fma_checker(fm_oracle):
+    """100 steps at N=128 (the reference main's parameters): bit for bit the
+    checker's fma time stepper, the same cycle counts."""
+    O = fm_oracle
+    g = load_golden("e2e_N128.npz")
+    N, maxlvl, nu, dt, T, tol = g["params"]
+    N, maxlvl = int(N), int(maxlvl)
+    u0, v1, v2 = init_problem(N)
+    want, cyc_ref = O.timestepper(u0, v1, v2, nu, maxlvl, N, dt, T, 1.0 / N, tol)
+    uT = np.empty_like(u0)
+    cyc = timestepper(uT, u0, v1, v2, nu, maxlvl, N, dt, T, 1.0 / N, tol, fp_mode=_lib.FP_FMA)
+    assert cyc == cyc_ref
+    assert np.array_equal(uT, want)

@@ -214,3 +214,25 @@ def test_slab_ops_equal_whole_field(oracle_mod, N, r0, nr):
     ps = O.prolongation_slab(u[sl].copy(), N, r0)
     I1 = min(2 * (r0 + nr - 1), 2 * N)
     assert np.array_equal(ps, pf[2 * r0 * W:(I1 + 1) * W])
+
+
+@pytest.mark.parametrize("tag", ["N32", "N64", "N128", "N128_nu001"])
+def test_fma_form_within_tolerance_of_reference(oracle_mod, tag):
+    """The checker's restatement of libmgx's fp_mode fma (or_set_fp_mode)
+    against the reference's own 100-step uT: max|duT| <= 1e-12 with the same
+    cycle counts -- the contracted form meets the stated
+    tolerance on the CPU as well; on the GPU the fma kernels equal this
+    restatement bit for bit (tests/test_gpu_fma.py)."""
+    O = oracle_mod
+    g = load_golden(f"e2e_{tag}.npz")
+    N, maxlvl, nu, dt, T, tol = g["params"]
+    N, maxlvl = int(N), int(maxlvl)
+    u0, v1, v2 = O.init_problem(N)
+    O.set_fp_mode(1)
+    try:
+        uT, cyc = O.timestepper(u0, v1, v2, nu, maxlvl, N, dt, T, 1.0 / N, tol)
+    finally:
+        O.set_fp_mode(0)
+    assert cyc == list(g["cycles"])
+    err = float(np.max(np.abs(uT - g["uT"])))
+    assert 0 < err <= 1e-12, err
