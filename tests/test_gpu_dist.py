@@ -346,3 +346,22 @@ def test_C4_two_timesteps_overlapped_N16384(golden_summary, overlap):
         u = mg.download(u0)
     assert cyc == [3, 3]
     assert hashlib.sha256(u.tobytes()).hexdigest() == s["sha256"]
+
+
+def test_overlap2_without_xfast_is_bitwise(overlap):
+    """Round-3 advisor finding: dist_overlap = 2 with the unguarded kernels
+    off (xfast = 0) has no split pass to run; the cross pass must then take
+    its plain form (not skip the finest level) -- bitwise the one-GPU result,
+    and no error."""
+    N, L, G = 4096, 7, 4
+    dt = 1.0 / N / 10
+    old = _lib.get_tuning("xfast")
+    try:
+        _lib.set_tuning("xfast", 0)
+        us, ns, rs, _ = _run(N, L, dt, NU, 3)
+        overlap(2)
+        up, npart, rp, info = _run(N, L, dt, NU, 3, parts=G)
+    finally:
+        _lib.set_tuning("xfast", old)
+    assert np.array_equal(up, us)
+    np.testing.assert_allclose(npart, ns, rtol=NORM_RTOL)

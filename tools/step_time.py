@@ -1,7 +1,7 @@
 """Time steps at N=16384, interleaved over the values of one tuning key
 (default step_fuse 0/1), and print one step's residual history.
     python tools/step_time.py [--N 16384 --L 9 --steps 3 --rounds 2
-                               --key post_predict --values 0,100]"""
+                               --key post_predict --values 0,100 --fp fma]"""
 import argparse, sys, time
 sys.path.insert(0, '.')
 import hpcclassmultigridproject_amd as pkg
@@ -13,11 +13,13 @@ ap.add_argument('--steps', type=int, default=3)
 ap.add_argument('--rounds', type=int, default=2)
 ap.add_argument('--key', default='step_fuse')
 ap.add_argument('--values', default='0,1')
+ap.add_argument('--fp', choices=['bitwise', 'fma'], default='bitwise')
 a = ap.parse_args()
 N, L = a.N, a.L
 vals = [int(v) for v in a.values.split(',')]
 u0, v1, v2 = pkg.init_problem(N, nthreads=16)
-mg = pkg.Multigrid(N, L, 1.0 / N / 10, -4e-4, device=0)
+mg = pkg.Multigrid(N, L, 1.0 / N / 10, -4e-4, device=0,
+                   fp_mode=_lib.FP_FMA if a.fp == 'fma' else _lib.FP_BITWISE)
 mg.upload(u0, v1, v2)
 mg.rhs()
 r0 = mg.residual_norm(0)
