@@ -120,6 +120,7 @@ struct Dist {
     // not run concurrently from two streams, those of two communicators may
     ncclComm_t comm_x = nullptr;
     double *hsum = nullptr;    // pinned
+    double *dsum_all = nullptr;   // virtual ranks: the parts' sums added (device)
     // dist_overlap: ghost exchanges on a second stream beside the interior pass
     hipStream_t xs = nullptr;
     hipEvent_t ev_fork = nullptr;
@@ -167,6 +168,7 @@ void dist_free(mgx_ctx *c) {
     for (hipEvent_t e : d->ev_lvl)
         if (e) (void)hipEventDestroy(e);
     if (d->hsum) (void)hipHostFree(d->hsum);
+    (void)hipFree(d->dsum_all);
     delete d;
     c->dist = nullptr;
 }
@@ -177,6 +179,7 @@ static int build_dist(mgx_ctx *c, int world, const std::vector<int> &ranks) {
     d->la = plan_la(c->N, c->L, world);
     for (int l = 0; l < d->la; ++l) CHK(plan_check(c->N, l, world));
     HIPCHK(hipHostMalloc(&d->hsum, sizeof(double) * 8));
+    HIPCHK(hipMalloc(&d->dsum_all, sizeof(double) * 8));
     // the zero row the marches read for zero velocity rows: the finest pitch
     (void)hipFree(c->zrow);
     c->zrow = nullptr;
@@ -221,6 +224,73 @@ static int build_dist(mgx_ctx *c, int world, const std::vector<int> &ranks) {
 }
 
 // ---------------------------------------------------------------- transport
+// Virtual ranks: all the row-block copies of one exchange (every part's ghost
+// rows to both neighbours, or the all-gather of the replicated level's rhs)
+// as ONE kernel instead of one blit launch per copy (G = 8: 14 per ghost
+// exchange, 56 per all-gather).  Workgroup b copies chunk b - first[k] of
+// copy k, 16 B per lane (the copies are whole pitched rows: 16-double
+// multiples, 128-B aligned).
+constexpr int kMaxCopies = 64;
+constexpr long kCopyChunk = 8192;   // doubles per workgroup
+struct CopyList {
+    const double *src[kMaxCopies];
+    double *dst[kMaxCopies];
+    long cnt[kMaxCopies];
+    int first[kMaxCopies + 1];   // prefix workgroup counts
+    int n;
+};
+
+__global__ __launch_bounds__(256) void k_copy_list(const CopyList L) {
+    const int b = blockIdx.x;
+    int k = 0;
+    while (k + 1 < L.n && b >= L.first[k + 1]) ++k;
+    const long i0 = (long)(b - L.first[k]) * kCopyChunk;
+    const long i1 = min(i0 + kCopyChunk, L.cnt[k]);
+    const double2 *src = reinterpret_cast<const double2 *>(L.src[k]);
+    double2 *dst = reinterpret_cast<double2 *>(L.dst[k]);
+    for (long i = i0 / 2 + threadIdx.x; i < i1 / 2; i += 256) dst[i] = src[i];
+}
+
+struct CopyBatch {
+    CopyList L{};
+    int blocks = 0;
+    int add(const double *src, double *dst, long cnt, hipStream_t st) {
+        if (cnt <= 0) return MGX_OK;
+        if ((cnt & 1) || ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15))
+            return fail(MGX_E_INTERNAL, "copy list: rows not 16-B aligned");
+        if (L.n == kMaxCopies) CHK(flush(st));
+        L.src[L.n] = src;
+        L.dst[L.n] = dst;
+        L.cnt[L.n] = cnt;
+        L.first[L.n] = blocks;
+        blocks += (int)((cnt + kCopyChunk - 1) / kCopyChunk);
+        L.first[++L.n] = blocks;
+        return MGX_OK;
+    }
+    int flush(hipStream_t st) {
+        if (L.n == 0) return MGX_OK;
+        hipLaunchKernelGGL(k_copy_list, dim3((unsigned)blocks), dim3(256), 0, st, L);
+        HIPCHK(hipGetLastError());
+        L.n = 0;
+        blocks = 0;
+        return MGX_OK;
+    }
+};
+
+// Virtual ranks: the parts' partial sums of squares added in part order (the
+// host loop's order: bitwise the same) on the device, one read-back.
+struct PtrList {
+    const double *p[kMaxCopies];
+    int n;
+};
+__global__ void k_sum_list(const PtrList L, double *out) {
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int i = 0; i < L.n; ++i) t += *L.p[i];
+        *out = t;
+    }
+}
+
 enum Field { kU, kRhs, kV1, kV2 };
 
 static double *field(const PLevel &L, Field f, int buf = -1) {
@@ -245,12 +315,9 @@ static int exchange_rows(mgx_ctx *c, const std::vector<XF> &xs, hipStream_t st) 
     std::vector<Xfer> plan;
     if (d->local) {
         // part i's send to j lands where j's plan receives from i (the plan is
-        // checked pairwise at context creation: plan_check).  On the side
-        // stream the copies go to the DMA engines (no compute units), as an
-        // interconnect transfer would: as blit kernels beside the level passes
-        // they took CUs from them (level 1 +10 % at G=8)
-        const hipMemcpyKind kind =
-            st == d->xs ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToDevice;
+        // checked pairwise at context creation: plan_check); all of them in
+        // one copy kernel (CopyBatch)
+        CopyBatch cb;
         for (const XF &x : xs)
             for (size_t i = 0; i < d->parts.size(); ++i) {
                 const PLevel &L = d->parts[i].lv[x.l];
@@ -258,13 +325,12 @@ static int exchange_rows(mgx_ctx *c, const std::vector<XF> &xs, hipStream_t st) 
                 ghost_plan(c->N, x.l, d->world, d->parts[i].rank, plan);
                 for (const Xfer &t : plan) {
                     PLevel &R = d->parts[t.peer].lv[x.l];
-                    HIPCHK(hipMemcpyAsync(field(R, x.f, x.buf) + (long)t.send_row * P,
-                                          field(L, x.f, x.buf) + (long)t.send_row * P,
-                                          sizeof(double) * (size_t)t.send_rows * P, kind,
-                                          st));
+                    CHK(cb.add(field(L, x.f, x.buf) + (long)t.send_row * P,
+                               field(R, x.f, x.buf) + (long)t.send_row * P,
+                               (long)t.send_rows * P, st));
                 }
             }
-        return MGX_OK;
+        return cb.flush(st);
     }
     Part &p = d->parts[0];
     ncclComm_t comm = st == d->xs ? d->comm_x : d->comm;
@@ -390,15 +456,16 @@ static int gather_rhs(mgx_ctx *c) {
     if (d->world > 1) {
         long row0, q;
         if (d->local) {
+            CopyBatch cb;
             for (auto &dst : d->parts)
                 for (auto &src : d->parts) {
                     if (&dst == &src) continue;
                     gather_rows(c->N, d->la, d->world, src.rank, &row0, &q);
                     const long P = dst.sub->lv[0].pitch, off = row0 * P;
-                    HIPCHK(hipMemcpyAsync(dst.sub->lv[0].rhs + off, src.sub->lv[0].rhs + off,
-                                          sizeof(double) * q * P, hipMemcpyDeviceToDevice,
-                                          c->stream));
+                    CHK(cb.add(src.sub->lv[0].rhs + off, dst.sub->lv[0].rhs + off, q * P,
+                               c->stream));
                 }
+            CHK(cb.flush(c->stream));
         } else {
             Part &p = d->parts[0];
             gather_rows(c->N, d->la, d->world, p.rank, &row0, &q);
@@ -418,12 +485,17 @@ static int reduce_norm(mgx_ctx *c, double *norm) {
     Dist *d = c->dist;
     double tot = 0.0;
     if (d->local) {
+        PtrList pl{};
         for (auto &p : d->parts) {
-            HIPCHK(hipMemcpyAsync(d->hsum, p.dsum, sizeof(double), hipMemcpyDeviceToHost,
-                                  c->stream));
-            HIPCHK(hipStreamSynchronize(c->stream));
-            tot += d->hsum[0];
+            if (pl.n == kMaxCopies) return fail(MGX_E_INTERNAL, "too many virtual ranks");
+            pl.p[pl.n++] = p.dsum;
         }
+        hipLaunchKernelGGL(k_sum_list, dim3(1), dim3(64), 0, c->stream, pl, d->dsum_all);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(d->hsum, d->dsum_all, sizeof(double), hipMemcpyDeviceToHost,
+                              c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        tot = d->hsum[0];
     } else {
         Part &p = d->parts[0];
         NCCLCHK(ncclAllReduce(p.dsum, p.dsum, 1, ncclDouble, ncclSum, d->comm, c->stream));
