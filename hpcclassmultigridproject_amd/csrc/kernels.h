@@ -75,9 +75,6 @@ enum : int { kModeZero = 1, kModeProlong = 2, kModeRestrict = 4, kModeNorm = 8 }
 // and the residual norm of uin against it goes to *norm_out -- a time step's
 // compute_rhs, mg_outer's initial norm and the first pre-smoothing in one pass.
 constexpr int kModeRhsNorm = 16;
-// Mode bit 32 (with kModeZero | kModeRestrict, row march): u is not stored --
-// the level's post-smoothing pass recomputes it (launch_xsmooth_re)
-constexpr int kModeNoStore = 32;
 struct SmoothArgs {
     const double *uin;
     double *uout;
@@ -140,28 +137,13 @@ struct XArgs {
     // count, no norm), phase 2 = the edge launch only, its partials written
     // after the first `partials_done` and the norm taken over both; 0 = both.
     int band = 0, phase = 0, partials_done = 0;
-    // rows >= vz of v1 and v2 are zero: read from zrow (as SmoothArgs)
-    const double *zrow = nullptr;
-    int vz = 0x7fffffff;
 };
 int launch_xsmooth(const XArgs &a, int sweeps, hipStream_t s);
-// A coarse level's post-smoothing pass that recomputes its pre-smoothing
-// (k_xsmooth RE, fp_mode fma, whole level): u_out = GS^k(P(uc) + GS^k(0))
-// on rhs, with the pre-smoothing pass run as kModeZero | kModeRestrict |
-// kModeNoStore.  Uses uin (ignored), upre (= u_out), rhs, v1, v2, uc,
-// pitchc, n, pitch, c, zrow, vz of `a`.  Returns 0, or -1 when unsupported.
-int launch_xsmooth_re(const XArgs &a, int sweeps, hipStream_t s);
-// whether a level of size n runs its passes as row marches (not LDS tiles)
-bool level_marches(long n);
 // whether launch_xsmooth supports rhs_next on a whole level of size n
 bool xstep_supported(long n);
 // Cross pass: 1 = interior strips run the unguarded march (default), 0 = all guarded.
 void set_xfast(long v);
 long get_xfast();
-// fp_mode fma: the cross pass on a row block of more than xtile_max_rows rows
-// as one masked launch (1, default) or the interior + edge launches (0)
-void set_xwhole(long v);
-long get_xwhole();
 void set_march_tile_rows(long v);
 long get_march_tile_rows();
 // Cross pass on row blocks of <= xtile_max_rows rows (default 4097): edges as

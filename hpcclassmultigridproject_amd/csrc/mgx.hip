@@ -377,81 +377,6 @@ static int op_cross(mgx_ctx *c, bool store_post, bool rs = false) {
     return MGX_OK;
 }
 
-// tuning key "xre": fma levels below the finest that run as row marches skip
-// storing their pre-smoothed u; the post-smoothing pass recomputes it
-// (k_xsmooth RE): 1 (default) or 0
-long g_xre = 0;
-
-static bool re_ok(mgx_ctx *c, int l) {
-    const Level &L = c->lv[l];
-    return g_xre != 0 && l >= 1 && l < c->L - 1 && L.coef.fm && c->opt.smoother == 0 &&
-           c->opt.shape == 1 && (c->opt.nsmooth == 2 || c->opt.nsmooth == 3) &&
-           c->opt.fuse >= c->opt.nsmooth && L.zero && mgx::level_marches(L.n);
-}
-
-// One visit of level l >= 1 in a V-cycle, fma (multigrid.cpp:69-88): the
-// pre-smoothing from zero + restriction WITHOUT storing u (kModeNoStore),
-// the coarser levels, then ONE pass that recomputes the same pre-smoothed u
-// in registers (bitwise: the same operations on the same rhs), adds the
-// prolongation of the coarse correction and post-smooths
-// (launch_xsmooth_re): the level's u_pre never goes through HBM (-1 write,
-// -1 read of the level's u per cycle).
-static int op_level_re(mgx_ctx *c, int l) {
-    Level &L = c->lv[l], &Cl = c->lv[l + 1];
-    const int k = c->opt.nsmooth;
-    mgx::SmoothArgs A{};
-    A.uin = L.u[L.cur];
-    A.uout = L.u[L.nxt()];
-    A.rhs = L.rhs;
-    A.v1 = L.v1;
-    A.v2 = L.v2;
-    A.zrow = c->zrow;
-    A.vz = L.vz;
-    A.n = L.n;
-    A.pitch = L.pitch;
-    A.c = L.coef;
-    A.uc = Cl.U();
-    A.rhsc = Cl.rhs;
-    A.pitchc = Cl.pitch;
-    A.partials = c->partials;
-    A.norm_out = c->dscal;
-    // algorithmic bytes as the plain passes; compulsory: rhs, v
-    // read, the coarse rhs written
-    int blocks = 0;
-    CHK(launch(c, MGX_K_GS, l, 40.0 * k * L.M() + 40.0 * L.M() + 24.0 * Cl.M(),
-               8.0 * (L.M() + 2.0 * L.Mv() + Cl.M()), [&] {
-                   blocks = mgx::launch_smooth(
-                       A, k, mgx::kModeZero | mgx::kModeRestrict | mgx::kModeNoStore, c->stream);
-               }));
-    if (blocks < 0) return fail(MGX_E_ARG, "launch_smooth: unsupported no-store pass");
-    Cl.zero = true;
-    CHK(op_vcycle(c, l + 1));
-    CHK(materialize(c, l + 1));
-    mgx::XArgs X;
-    X.upre = L.u[L.nxt()];
-    X.rhs = L.rhs;
-    X.v1 = L.v1;
-    X.v2 = L.v2;
-    X.zrow = c->zrow;
-    X.vz = L.vz;
-    X.uc = Cl.U();
-    X.pitchc = Cl.pitch;
-    X.partials = c->partials;
-    X.n = L.n;
-    X.pitch = L.pitch;
-    X.c = L.coef;
-    X.store_post = false;
-    // compulsory: rhs, v and the coarse u read, u written
-    int rc = 0;
-    CHK(launch(c, MGX_K_PSMOOTH, l, 32.0 * L.M() + 40.0 * k * L.M() + 8.0 * Cl.M(),
-               8.0 * (2.0 * L.M() + 2.0 * L.Mv() + Cl.M()),
-               [&] { rc = mgx::launch_xsmooth_re(X, k, c->stream); }));
-    if (rc < 0) return fail(MGX_E_ARG, "launch_xsmooth_re: unsupported level");
-    L.cur = L.nxt();
-    L.zero = false;
-    return MGX_OK;
-}
-
 // mg_inner (multigrid.cpp:17-92).  If norm != nullptr (finest level only) the
 // residual norm after the cycle (multigrid.cpp:112-113) is produced too, fused
 // into the last post-smoothing pass when possible.
@@ -509,8 +434,6 @@ int op_vcycle(mgx_ctx *c, int l, double *norm, bool store_post) {
         const bool last = sh == c->opt.shape - 1;
         if (l == c->L - 1) {
             CHK(op_coarse(c, l));
-        } else if (!norm && re_ok(c, l)) {
-            CHK(op_level_re(c, l));
         } else {
             CHK(op_smooth(c, l, c->opt.nsmooth, false, /*restrict=*/true, false, nullptr));
             CHK(op_vcycle(c, l + 1));
@@ -1440,16 +1363,6 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgxi::g_dist_min_rows = value;
         return MGX_OK;
     }
-    if (!strcmp(key, "xre")) {
-        if (value != 0 && value != 1) return fail(MGX_E_ARG, "xre must be 0 or 1");
-        g_xre = value;
-        return MGX_OK;
-    }
-    if (!strcmp(key, "xwhole")) {
-        if (value != 0 && value != 1) return fail(MGX_E_ARG, "xwhole must be 0 or 1");
-        mgx::set_xwhole(value);
-        return MGX_OK;
-    }
     if (!strcmp(key, "xfast")) {
         if (value != 0 && value != 1) return fail(MGX_E_ARG, "xfast must be 0 or 1");
         mgx::set_xfast(value);
@@ -1544,14 +1457,6 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "dist_min_rows")) {
         *value = mgxi::g_dist_min_rows;
-        return MGX_OK;
-    }
-    if (!strcmp(key, "xre")) {
-        *value = g_xre;
-        return MGX_OK;
-    }
-    if (!strcmp(key, "xwhole")) {
-        *value = mgx::get_xwhole();
         return MGX_OK;
     }
     if (!strcmp(key, "xfast")) {

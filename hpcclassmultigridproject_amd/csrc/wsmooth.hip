@@ -374,8 +374,8 @@ __global__ __launch_bounds__(64 * WPB, (WCfg<K, MODE>::MINB)) void k_wsmooth(
                         }
                     }
                 }
-                // (3) row s+2-S is final (kModeNoStore: recomputed later)
-                if (!(MODE & 32)) {
+                // (3) row s+2-S is final
+                {
                     const int ro = s + 2 - S;
                     st2_if(uout + rowoff(ro, ip), c0, rowin(ro) && keep,
                            ur[(p + 2 - S + 2 * NR) % NR]);
@@ -695,7 +695,6 @@ static int smooth_winst(const SmoothArgs &A, hipStream_t s) {
 long g_tile_max_n = 1024;
 void set_tile_max_n(long v) { g_tile_max_n = v; }
 long get_tile_max_n() { return g_tile_max_n; }
-bool level_marches(long n) { return n > g_tile_max_n; }
 long g_tile32_min_n = 2048;   // 32-row tiles on levels n >= this (tuning key "tile32_min_n")
 void set_tile32_min_n(long v) { g_tile32_min_n = v; }
 long get_tile32_min_n() { return g_tile32_min_n; }
@@ -780,7 +779,6 @@ static int smooth_k(const SmoothArgs &A, int mode, hipStream_t s) {
         case 9: return smooth_block<K, 9>(A, s);
         case 10: return smooth_block<K, 10>(A, s);
         case 20: return smooth_block<K, 20>(A, s);
-        case 37: return smooth_winst<4, K, 37>(A, s);   // (row march only)
         default: return -1;
     }
 }

@@ -32,14 +32,6 @@ namespace {
 #ifndef MGX_XU
 #define MGX_XU 2
 #endif
-// the recompute pass (RE: t1 / t2 rows from HBM, not factors) prefetches its
-// rhs / v rows fewer steps ahead: each step in flight is 6 doubles per lane
-#ifndef MGX_XRV_RE
-#define MGX_XRV_RE 3
-#endif
-#ifndef MGX_XU_RE
-#define MGX_XU_RE 1
-#endif
 #ifndef MGX_XACOEF
 #define MGX_XACOEF 1
 #endif
@@ -47,12 +39,11 @@ namespace {
 #ifndef MGX_XEDGE_ROWS
 #define MGX_XEDGE_ROWS 16
 #endif
-template <int K, bool RE = false>
+template <int K>
 struct XCfg {
     static constexpr int S = 2 * K;
-    // (RE: no residual stages)
-    static constexpr int EB = RE ? S : S + 1;    // B: stages + restriction residual
-    static constexpr int EA = RE ? S : S + 1;    // A: stages + norm residual
+    static constexpr int EB = S + 1;             // B: stages + restriction residual
+    static constexpr int EA = S + 1;             // A: stages + norm residual
     static constexpr int H = (S + EB + 1) / 2;   // halo pairs per side
     static constexpr int NR = S + 4;             // register rings / unroll period
     static constexpr int W = 2 * (64 - 2 * H);
@@ -108,28 +99,7 @@ struct XCfg {
 // contracted update (one fma each), every update is four fmas and every
 // residual d*(update - u).  B's time-step rhs (RS) keeps the reference
 // expressions (gs.cpp:44, stored unscaled) and is scaled after.
-//
-// MK = true (with FM, G = false): the whole row block in ONE launch, no edge
-// kernel.  The boundary points keep their values through their coefficients
-// instead of guards: a point on row 0 or n (or any row outside [1, n-1]), or
-// on column 0 or n (the x point of its lane: c0 is even), or left / right of
-// the grid gets m = 0 and f' = u, so its update u = f' + sum m*u returns u
-// exactly, in the same stage chain as every other point (the row's
-// coefficients are formed once per row: a few more VALU per row, none per
-// stage).  An interior point's m and f' are bitwise the unmasked ones (g*1,
-// fma(f, rdgs*1, u*0) = fl(f*rdgs)).  The points right of column n (lanes
-// past the grid's last column) and the rows outside [0, n] hold garbage that
-// only ever feeds those fixed boundary points; norms, restriction and rhs
-// stores test the boundary as the guarded kernel does (once per row).
-//
-// RE = true (a coarse level's post-smoothing, mgx.hip op_level_re): A runs
-// the level's PRE-smoothing again, from zero (multigrid.cpp:77) on the rhs --
-// bitwise the pass whose u it did not store -- and adds the prolongation of
-// the coarser level's correction (gs.cpp:238-265) to each final u row on its
-// way to B; B runs the post-smoothing and stores u.  No norm, no
-// restriction: the level's u_pre is never written to nor read from HBM.
-template <int WPB, int K, bool G, bool RS = false, bool SV = false, bool FM = false,
-          bool MK = false, bool RE = false>
+template <int WPB, int K, bool G, bool RS = false, bool SV = false, bool FM = false>
 __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     const double *__restrict__ uin, double *__restrict__ upost, double *__restrict__ upre,
     const double *__restrict__ rhs, const double *__restrict__ v1, const double *__restrict__ v2,
@@ -138,9 +108,8 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     int lo, int hi, int store_post, double *__restrict__ rhs_next,
     double *__restrict__ partials2, const double *__restrict__ sa1,
     const double *__restrict__ sb1, const double *__restrict__ sa2,
-    const double *__restrict__ sb2, const double *__restrict__ zrow, int vz) {
-    using X = XCfg<K, RE>;
-    static_assert(!RE || (!RS && !SV), "the recompute pass: coarse levels, cycles only");
+    const double *__restrict__ sb2) {
+    using X = XCfg<K>;
     constexpr int S = X::S, H = X::H, NR = X::NR, W = X::W, D = X::D, NU = X::NU,
                   NRD = X::NRD, EA = X::EA, EB = X::EB;
     // A's prefetch distances in steps: rhs/v rows XRV ahead of their first
@@ -148,13 +117,12 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     // pass is bound by loads in flight, not by VALU: rhs/v 2 -> 3 -> 4 steps
     // took level 0 -4 % and -3 % at the same VGPR count (B's path sets it);
     // u 3-4 steps or rhs/v 5 measured no better (N=16384, tools/ab_libs.sh).
-    constexpr int XRV = RE ? MGX_XRV_RE : MGX_XRV;
-    constexpr int XU = RE ? MGX_XU_RE : MGX_XU;
+    constexpr int XRV = MGX_XRV;
+    constexpr int XU = MGX_XU;
     // A forms each row's coefficients once (MGX_XACOEF; B always does).  Not
     // in the guarded edge kernel: there it takes the kernel past 256 VGPRs
     // (one wave per SIMD), and the edge launch is latency bound
-    constexpr bool XACOEF = MK || (MGX_XACOEF != 0 && !G);
-    static_assert(!MK || (FM && !G), "the masked whole-block form is the fma unguarded kernel");
+    constexpr bool XACOEF = MGX_XACOEF != 0 && !G;
     static_assert(XU >= 1 && XU <= NR - 3, "u prefetch distance");
     // row s+XRV takes the ring slot of row s+XRV-NR, last used by A's norm of
     // row s+1-S
@@ -189,9 +157,6 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
         auto own = [&](const int r) { return (unsigned)(r - a) < (unsigned)(b - a) && keep; };
         const bool in0 = act && c0 >= 1 && c0 <= n - 1;
         const bool in1 = act && c0 + 1 <= n - 1;
-        const double wlx = in0 ? 1.0 : 0.0;   // MK: the lane's x point updatable (columns)
-        // MK: the boundary test of row r (wave-uniform)
-        auto inrow = [&](const int r) { return r >= 1 && r <= n - 1; };
         const int cl = min(max(c0, 0), (int)pitch - 2);
         const int jl = cl >> 1;
         const int j1 = (jl + 1 <= nc) ? 1 : 0;
@@ -215,10 +180,9 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
         }
         // A: u row R + its coarse parents (odd = R's parity, compile-time:
         // an even row needs only the coarse row below it)
-        // (RE: the coarse parents only, of the row A hands to B XU steps later)
         auto load_u = [&](int R, UPre &u, const bool odd) {
             const int Rc = min(max(R, lo), hi);
-            if (!RE) u.X = ld2u(uin + rowoff(Rc, ip), bcl);
+            u.X = ld2u(uin + rowoff(Rc, ip), bcl);
             const double *p0 = uc + rowoff(Rc >> 1, ipc);
             u.q00 = ld1u(p0, bjl);
             u.q01 = ld1u(p0, bjl1);
@@ -228,8 +192,9 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                 u.q11 = ld1u(p1, bjl1);
             }
         };
-        // v + prolongation (gs.cpp:238-265); static parity, select (see k_wsmooth)
-        auto prol = [&](int R, const UPre &u, const bool odd, double2 v) {
+        // + prolongation (gs.cpp:238-265); static parity, select (see k_wsmooth)
+        auto make_u = [&](int R, const UPre &u, const bool odd) {
+            double2 v = u.X;
             double2 pv;
             const double q01 = (!GM || j1) ? u.q01 : 0.0;
             const double q11 = (!GM || j1) ? u.q11 : 0.0;
@@ -244,11 +209,6 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             v.x = on ? v.x + pv.x : v.x;
             v.y = on ? v.y + pv.y : v.y;
             return v;
-        };
-        // A: u row R as it enters the ring (RE: zero, multigrid.cpp:77)
-        auto make_u = [&](int R, const UPre &u, const bool odd) {
-            if (RE) return make_double2(0.0, 0.0);
-            return prol(R, u, odd, u.X);
         };
         // SV: the lane's column factors scaled by h/2 (exact), and a ring of
         // row factors (wave-uniform: SGPRs), slot q = the rd slot of the row
@@ -269,34 +229,20 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             if (SV) {   // (32-bit byte offsets: the scalar loads' SGPR-offset form)
                 ar1[q] = *reinterpret_cast<const double *>(rowb(sa1, (unsigned)Rc * 8u));
                 ar2[q] = *reinterpret_cast<const double *>(rowb(sa2, (unsigned)Rc * 8u));
-            } else {   // (RE: rows >= vz are zero, read from the L2-resident zero row)
-                const bool z = RE && Rc >= vz;
-                const double2 x = ld2((z ? zrow : v1 + o) + cl), y = ld2((z ? zrow : v2 + o) + cl);
+            } else {
+                const double2 x = ld2((v1 + o) + cl), y = ld2((v2 + o) + cl);
                 d.x = make_double2(x.x * hh, x.y * hh);
                 d.y = make_double2(y.x * hh, y.y * hh);
             }
         };
         // A, the row in slot q at its first stage: t from the factors (SV),
         // and f' = f/d (FM)
-        // (MK: f' = u on the boundary points of row r, the row's u in ur[q])
-        auto scale_f = [&](double2 &f, const double2 u, const int r) {
-            if (!MK) {
-                f = make_double2(f.x * c.rdgs, f.y * c.rdgs);
-                return;
-            }
-            const bool ir = inrow(r);
-            double wx = ir ? wlx : 0.0;
-            asm volatile("" : "+v"(wx));   // no hoisted per-lane products
-            const double ry = ir ? c.rdgs : 0.0, oy = ir ? 0.0 : 1.0;
-            f = make_double2(__builtin_fma(f.x, c.rdgs * wx, u.x * (1.0 - wx)),
-                             __builtin_fma(f.y, ry, u.y * oy));
-        };
-        auto first_use = [&](const int q, const int r) {
+        auto first_use = [&](const int q) {
             if (SV) {
                 rd[q].x = make_double2(ar1[q] * bh1.x, ar1[q] * bh1.y);
                 rd[q].y = make_double2(ar2[q] * bh2.x, ar2[q] * bh2.y);
             }
-            if (FM) scale_f(rd[q].r, ur[q], r);
+            if (FM) rd[q].r = make_double2(rd[q].r.x * c.rdgs, rd[q].r.y * c.rdgs);
         };
         // one red-black stage h of the march step at row phase p on row r,
         // the coefficients from t (A's stages in the guarded kernel)
@@ -369,19 +315,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             const double2 z = make_double2(0.0, 0.0);
             cf[i] = CoefRow{z, z, z, z};
         }
-        auto to_coef = [&](const RowData &d, CoefRow &k, const int r) {
-            if (MK) {   // m = 0 on the boundary points of row r
-                const bool ir = inrow(r);
-                double wx = ir ? wlx : 0.0;
-                asm volatile("" : "+v"(wx));   // no hoisted per-lane products
-                const double gx = c.g * wx, gnx = c.gn * wx, c2x = c.c2 * wx;
-                const double gy = ir ? c.g : 0.0, gny = ir ? c.gn : 0.0, c2y = ir ? c.c2 : 0.0;
-                k.cn = make_double2(__builtin_fma(gx, d.x.x, -gnx), __builtin_fma(gy, d.x.y, -gny));
-                k.cw = make_double2(__builtin_fma(gx, d.y.x, -gnx), __builtin_fma(gy, d.y.y, -gny));
-                k.cs = make_double2(c2x - k.cn.x, c2y - k.cn.y);
-                k.ce = make_double2(c2x - k.cw.x, c2y - k.cw.y);
-                return;
-            }
+        auto to_coef = [&](const RowData &d, CoefRow &k) {
             if (FM) {
                 k.cn = make_double2(fm_mp(d.x.x, c), fm_mp(d.x.y, c));
                 k.cw = make_double2(fm_mp(d.y.x, c), fm_mp(d.y.y, c));
@@ -437,14 +371,11 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
         if (isA) {
 #pragma unroll
             for (int d = 0; d < 3; ++d) {
-                if (!RE) load_u(s0 + d, up[d], d & 1);
+                load_u(s0 + d, up[d], d & 1);
                 ur[d] = make_u(s0 + d, up[d], d & 1);
             }
-            // the u rows (RE: the hand-off rows' coarse parents) XU ahead
-            constexpr int LU = RE ? 2 - S : 3;
 #pragma unroll
-            for (int d = LU; d < LU + XU; ++d)
-                load_u(s0 + d, up[(d + 2 * NR) % NR], d & 1);
+            for (int d = 3; d < 3 + XU; ++d) load_u(s0 + d, up[d], d & 1);
 #pragma unroll
             for (int d = 1; d < XRV; ++d) load_rv(s0 + d, d);
             for (;;) {
@@ -452,13 +383,12 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                 for (int p = 0; p < NR; ++p) {   // s == p (mod NR)
                     const int s = s0 + it + (p & 1);
                     ur[(p + 3) % NR] = make_u(s + 3, up[(p + 3) % NR], (p + 3) & 1);
-                    load_u(s + LU + XU, up[(p + LU + XU + 2 * NR) % NR],
-                           (p + LU + XU) & 1);   // XU ahead
-                    first_use((p + 1) % NR, s + 1);   // row s+1: first used by stage 0 below
+                    load_u(s + 3 + XU, up[(p + 3 + XU) % NR], (p + 3 + XU) & 1);   // XU ahead
+                    first_use((p + 1) % NR);   // row s+1: first used by stage 0 below
                     if (XACOEF) {
                         // the row's four coefficients once (as B does), not in
                         // each of its point's stages
-                        to_coef(rd[(p + 1) % NR], cf[(p + 1) % NR], s + 1);
+                        to_coef(rd[(p + 1) % NR], cf[(p + 1) % NR]);
 #pragma unroll
                         for (int h = 0; h < S; ++h) stage_c(p, h, s + 1 - h);
                     } else {
@@ -475,18 +405,14 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                     }
                     {
                         const int ro = s + 2 - S;
-                        double2 uf = ur[(p + 2 - S + 2 * NR) % NR];
-                        // RE: + the prolongation, for B's post-smoothing (A's
-                        // ring keeps the pre-smoothed row: a neighbour still)
-                        if (RE)
-                            uf = prol(ro, up[(p + 2 - S + 2 * NR) % NR], (p + 2 - S) & 1, uf);
+                        const double2 uf = ur[(p + 2 - S + 2 * NR) % NR];
                         uring[pr][(p + 2 - S + 2 * NR) % NU][l] = uf;
-                        if (!RE) st2_ifu(upost + rowoff(ro, ip), c0, post && own(ro), uf);
+                        st2_ifu(upost + rowoff(ro, ip), c0, post && own(ro), uf);
                     }
                     // residual norm of u_post (multigrid.cpp:112-113), column c0 of
                     // row s+1-S (its neighbours are final now; B takes column c0+1:
                     // half each balances the pair's VALU work)
-                    if (!RE) {
+                    {
                         const int r = s + 1 - S;
                         const int iR = (p + 1 - S + 2 * NR) % NR;
                         const int iN = (p - S + 2 * NR) % NR;
@@ -504,7 +430,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                             }
                         } else {   // acc + 0.0 == acc (acc >= +0): a select, no branch
                             const double r0 = res0();
-                            acc += (own(r) && (!MK || (inrow(r) && in0))) ? r0 * r0 : 0.0;
+                            acc += own(r) ? r0 * r0 : 0.0;
                         }
                     }
                     load_rv(s + XRV, (p + XRV) % NR);
@@ -534,7 +460,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                     // residual norm of u_post (multigrid.cpp:112-113) on row s+2,
                     // column c0+1 (A takes c0): rows s+1..s+3 are still untouched
                     // u_post here
-                    if (!RE) {
+                    {
                         const int r = s + 2;
                         const int iR = (q + 2) % NR, iN = (q + 1) % NR, iS = (q + 3) % NR;
                         const double uE = dpp_shl1(ur[iR].x);
@@ -545,7 +471,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                             }
                         } else {   // acc + 0.0 == acc (acc >= +0): a select, no branch
                             const double r1 = res_ty(iR, iN, iS, uE);
-                            acc += (own(r) && (!MK || (inrow(r) && in1))) ? r1 * r1 : 0.0;
+                            acc += own(r) ? r1 * r1 : 0.0;
                         }
                     }
                     if (RS) {
@@ -565,8 +491,8 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         const double f1 = rhs_point_t(d.x.y, d.y.y, ur[iR].y, ur[iN].y, ur[iR].x,
                                                       ur[iS].y, uE, cg);
                         d.r = make_double2(f0, f1);
-                        const bool i0 = !(GN || MK) || (r >= 1 && r <= n - 1 && in0);
-                        const bool i1 = !(GN || MK) || (r >= 1 && r <= n - 1 && in1);
+                        const bool i0 = !GN || (r >= 1 && r <= n - 1 && in0);
+                        const bool i1 = !GN || (r >= 1 && r <= n - 1 && in1);
                         double *row = rhs_next + rowoff(r, ip);
                         if (own(r)) {
                             if (i0 && i1) {
@@ -582,9 +508,9 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                                                       ur[iR].x, ur[iS].y, uE, cg);
                         acc2 += (own(r) && i0) ? e0 * e0 : 0.0;
                         acc2 += (own(r) && i1) ? e1 * e1 : 0.0;
-                        if (FM) scale_f(d.r, ur[iR], r);
+                        if (FM) d.r = make_double2(f0 * c.rdgs, f1 * c.rdgs);
                     }
-                    to_coef(rd[(q + 1) % NR], cf[(q + 1) % NR], s + 1);   // row s+1
+                    to_coef(rd[(q + 1) % NR], cf[(q + 1) % NR]);   // row s+1
 #pragma unroll
                     for (int h = 0; h < S; ++h) stage_c(q, h, s + 1 - h);
                     {
@@ -592,15 +518,15 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         st2_ifu(upre + rowoff(ro, ip), c0, own(ro),
                                 ur[(q + 2 - S + 2 * NR) % NR]);
                     }
-                    if (!RE && ((q + 1 - S) & 1) == 0) {   // compile-time row parity
+                    if (((q + 1 - S) & 1) == 0) {   // compile-time row parity
                         // residual -> coarse rhs at the even-even points (:73-75)
                         const int r = s + 1 - S;
                         const int iR = (q + 1 - S + 2 * NR) % NR;
                         const int iN = (q - S + 2 * NR) % NR;
                         const int iS = (q + 2 - S + 2 * NR) % NR;
                         const double uW = dpp_shr1(ur[iR].y);
-                        const bool on = own(r) && (!(GN || MK) ||
-                                                   (r >= 1 && r <= n - 2 && in0 && c0 <= n - 2));
+                        const bool on = own(r) &&
+                                        (!GN || (r >= 1 && r <= n - 2 && in0 && c0 <= n - 2));
                         const double res = res_x(iR, iN, iS, uW);
                         st1_ifu(rhsc + rowoff(r >> 1, ipc), c0 >> 1, on, res);
                     }
@@ -624,7 +550,6 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
         if (__builtin_amdgcn_readfirstlane(strip) >= 0)
             march(strip * W - 2 * H, strip * W, strip * W + W, a, b);
     }
-    if (RE) return;
     const double tot = wave_sum(acc);   // one partial per wave (A: columns c0, B: c0+1)
     if (l == 0) partials[(long)blockIdx.x * 2 * WPB + wv] = tot;
     if (RS) {
@@ -879,12 +804,8 @@ __global__ __launch_bounds__(256) void k_xtile(
 long g_xfast = 1;   // unguarded interior march kernels (tuning key "xfast")
 void set_xfast(long v) { g_xfast = v; }
 long get_xfast() { return g_xfast; }
-// fma passes on long row blocks as one masked launch (tuning key "xwhole")
-long g_xwhole = 0;
-void set_xwhole(long v) { g_xwhole = v; }
-long get_xwhole() { return g_xwhole; }
 
-template <int WPB, int K, bool G, bool RS, bool SV, bool FM, bool MK, bool RE>
+template <int WPB, int K, bool G, bool RS, bool SV, bool FM>
 static int xsmooth_slots() {
     static int slots = 0;   // resident workgroups of this instantiation
     if (!slots) {
@@ -892,7 +813,7 @@ static int xsmooth_slots() {
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per,
-                                                           k_xsmooth<WPB, K, G, RS, SV, FM, MK, RE>,
+                                                           k_xsmooth<WPB, K, G, RS, SV, FM>,
                                                            128 * WPB, 0);
         slots = std::max(1, cus) * std::max(1, per);
     }
@@ -902,23 +823,22 @@ static int xsmooth_slots() {
 // One launch over `reg`; min_rows: the fewest rows per workgroup (each
 // workgroup's march pays a warm-up of ~EA + EB + D rows).  Returns the norm
 // partials written (grid * 2 * WPB: one per wave) at `partials`.
-template <int WPB, int K, bool G, bool RS, bool SV, bool FM, bool MK = false, bool RE = false>
+template <int WPB, int K, bool G, bool RS, bool SV, bool FM>
 static int xsmooth_launch_sv(const XArgs &A, const MarchRegions &reg, double *partials, int lo,
                              int hi, long min_rows, long max_wgs, hipStream_t s) {
     const long total = reg.pre[reg.count];
     if (total <= 0) return 0;
     long upw;
     MarchRegions r;
-    using X = XCfg<K, RE>;
-    const unsigned grid = plan_march(reg, WPB, xsmooth_slots<WPB, K, G, RS, SV, FM, MK, RE>(), min_rows,
+    using X = XCfg<K>;
+    const unsigned grid = plan_march(reg, WPB, xsmooth_slots<WPB, K, G, RS, SV, FM>(), min_rows,
                                      max_wgs, X::EA + X::EB + X::D + X::NR / 2, upw, r);
     // RS: the second partials (the next step's initial norm) at the same
     // offsets, kNormBlocks further on
-    MGX_LAUNCH((k_xsmooth<WPB, K, G, RS, SV, FM, MK, RE>), dim3(grid), dim3(128 * WPB), s, A.uin,
+    MGX_LAUNCH((k_xsmooth<WPB, K, G, RS, SV, FM>), dim3(grid), dim3(128 * WPB), s, A.uin,
                A.upost, A.upre, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n,
                A.pitch, r, upw, A.c, lo, hi, A.store_post ? 1 : 0, A.rhs_next,
-               RS ? partials + kNormBlocks : (double *)nullptr, A.sa1, A.sb1, A.sa2, A.sb2,
-               A.zrow ? A.zrow : A.v1, A.zrow ? A.vz : 0x7fffffff);
+               RS ? partials + kNormBlocks : (double *)nullptr, A.sa1, A.sb1, A.sa2, A.sb2);
     return (int)grid * 2 * WPB;
 }
 // SV when the level's velocity factors are given (XArgs::sa1); FM = the
@@ -939,20 +859,6 @@ static int xsmooth_launch(const XArgs &A, const MarchRegions &reg, double *parti
                                                             max_wgs, s);
     return xsmooth_launch_sv<WPB, K, G, RS, false, false>(A, reg, partials, lo, hi, min_rows,
                                                          max_wgs, s);
-}
-
-// fma: the whole row block [ra, rb) as ONE launch of the masked unguarded
-// kernel (k_xsmooth MK): every strip and row, no edge launch.
-template <int WPB, int K, bool RS>
-static int xsmooth_whole(const XArgs &A, int ra, int rb, int lo, int hi, hipStream_t s) {
-    using X = XCfg<K>;
-    MarchRegions all, unused;
-    march_regions<WPB>(A.n, X::W, X::H, ra, rb, 0, 0, false, unused, all);
-    if (A.sa1 && A.sb1 && A.sa2 && A.sb2)
-        return xsmooth_launch_sv<WPB, K, false, RS, true, true, true>(
-            A, all, A.partials, lo, hi, A.min_rows, kNormBlocks / (2 * WPB) / 2, s);
-    return xsmooth_launch_sv<WPB, K, false, RS, false, true, true>(
-        A, all, A.partials, lo, hi, A.min_rows, kNormBlocks / (2 * WPB) / 2, s);
 }
 
 static void add_tile_region(TileRegions &r, int c0, int c1, int r0, int r1, int TR) {
@@ -1054,7 +960,6 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
         // (the caller checks xstep_supported first)
         if (g_xfast == 0 || !(A.c.dgs > 0) || A.rb >= 0 || rb - ra <= g_xtile_max_rows)
             return -3;
-        if (g_xwhole && A.c.fm) return xsmooth_whole<WPB, K, true>(A, ra, rb, lo, hi, s);
         MarchRegions inner, edge, unused;
         march_regions<WPB>(n, X::W, X::H, ra, rb, X::TOP_RS, X::BOT, true, inner, unused);
         march_regions<1>(n, X::W, X::H, ra, rb, X::TOP_RS, X::BOT, true, unused, edge);
@@ -1074,8 +979,6 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
     // the unguarded kernel's division assumes d > 0 (div_diag<true>)
     const bool split = g_xfast != 0 && A.c.dgs > 0;
     if (A.phase != 0 && !split) return -1;   // a split pass needs the split kernels
-    if (split && g_xwhole && A.c.fm && A.phase == 0 && rb - ra > g_xtile_max_rows)
-        return xsmooth_whole<WPB, K, false>(A, ra, rb, lo, hi, s);
     if (split && rb - ra <= g_xtile_max_rows) {
         const int r = xsmooth_tiled<WPB, K>(A, ra, rb, lo, hi, s);
         if (r != -2) return r;
@@ -1112,27 +1015,6 @@ int launch_xsmooth(const XArgs &A, int sweeps, hipStream_t s) {
     if (blocks > 0 && A.rhs_next)   // the next step's initial norm
         launch_norm_final(A.partials + kNormBlocks, blocks, A.norm2_out, 1, s);
     return blocks;
-}
-
-int launch_xsmooth_re(const XArgs &A, int sweeps, hipStream_t s) {
-    if (!A.c.fm || A.rb >= 0 || A.sa1) return -1;
-    const int ra = 0, rb = (int)A.n + 1, lo = 0, hi = (int)A.n;
-    MarchRegions all, unused;
-    switch (sweeps) {
-        case 2:
-            march_regions<4>(A.n, XCfg<2, true>::W, XCfg<2, true>::H, ra, rb, 0, 0, false, unused,
-                             all);
-            xsmooth_launch_sv<4, 2, false, false, false, true, true, true>(
-                A, all, A.partials, lo, hi, A.min_rows, kNormBlocks / 8 / 2, s);
-            return 0;
-        case 3:
-            march_regions<4>(A.n, XCfg<3, true>::W, XCfg<3, true>::H, ra, rb, 0, 0, false, unused,
-                             all);
-            xsmooth_launch_sv<4, 3, false, false, false, true, true, true>(
-                A, all, A.partials, lo, hi, A.min_rows, kNormBlocks / 8 / 2, s);
-            return 0;
-        default: return -1;
-    }
 }
 
 bool xstep_supported(long n) {

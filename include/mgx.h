@@ -197,16 +197,6 @@ int mgx_synchronize(mgx_ctx *ctx);
  * "xfast": 1 (default) runs the cross-cycle pass as an unguarded kernel over
  * the interior strips and rows plus a guarded kernel over the boundary strips
  * and bands; 0 = one guarded launch (bitwise the same results).
- * "xwhole": fp_mode fma only: 1 runs the cross-cycle pass on a row
- * block of more than xtile_max_rows rows as ONE launch of the unguarded kernel
- * whose boundary points keep their values through their coefficients (m = 0,
- * f' = u) -- no edge launch; 0 (default) = the xfast launches.  Bitwise the
- * same.
- * "xre": fp_mode fma only: 1 = a level below the finest whose passes
- * are row marches does not store its pre-smoothed u; its post-smoothing pass
- * recomputes it from the rhs (in registers, bitwise) before adding the
- * prolongation -- one write and one read of the level's u fewer per V-cycle;
- * 0 (default) = the stored form.  Bitwise the same.
  * "march_tile_rows": a row block whose wave march would give each resident
  * workgroup fewer than this many rows runs as LDS tiles (default 16, >= 0).
  * "xtile_max_rows": on row blocks of at most this many rows (a rank of a

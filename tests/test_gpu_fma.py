@@ -144,70 +144,6 @@ def test_fma_tiles_equal_marches(tile_max_n):
     assert np.array_equal(u, ref)
 
 
-@pytest.mark.parametrize("N,L,kw,steps,parts", [
-    (8192, 8, {}, 0, 0),                      # cycles: the cross pass
-    (4096, 7, dict(nsmooth=2), 0, 0),         # K=2 (xtile_max_rows 0: marched)
-    (8192, 8, {}, 2, 0),                      # time steps: the step-cross pass
-    (16384, 9, {}, 0, 2),                     # row blocks of a partitioned level 0
-    (16384, 9, dict(sep_velocity=0), 0, 0),   # tuning: v1 / v2 read from HBM
-])
-def test_fma_whole_launch_equals_split(N, L, kw, steps, parts):
-    """xwhole 1 (fma: the cross pass as ONE launch whose boundary points keep
-    their values through m = 0, f' = u) is bitwise the interior + edge
-    launches (xwhole 0)."""
-    kw = dict(kw)
-    tune = {k: kw.pop(k) for k in list(kw) if k in ("sep_velocity",)}
-    old = {k: _lib.get_tuning(k) for k in ("xwhole", "xtile_max_rows", *tune)}
-    out = {}
-    try:
-        for k, v in tune.items():
-            _lib.set_tuning(k, v)
-        if N <= 4096:
-            _lib.set_tuning("xtile_max_rows", 0)
-        for xw in (0, 1):
-            _lib.set_tuning("xwhole", xw)
-            if steps:
-                out[xw] = _steps(N, L, steps, _lib.FP_FMA, **kw)
-            else:
-                out[xw] = _cycles(N, L, 3, _lib.FP_FMA, parts=parts, **kw)
-    finally:
-        for k, v in old.items():
-            _lib.set_tuning(k, v)
-    assert np.array_equal(out[1][0], out[0][0])
-    # (steps: cycle counts; cycles: norms, whose partial sums follow the launch)
-    np.testing.assert_allclose(out[1][1], out[0][1], rtol=1e-12)
-
-
-@pytest.mark.parametrize("N,L,kw,steps", [
-    (16384, 9, {}, 0),                 # levels 1-3 march: each recomputes its u_pre
-    (8192, 8, dict(nsmooth=2), 0),     # K = 2
-    (8192, 8, {}, 2),                  # time steps (mg_outer's cycles)
-    (4096, 7, dict(sep_velocity=0), 0),
-])
-def test_fma_recompute_equals_stored(N, L, kw, steps):
-    """xre 1 (a marching coarse level skips storing its pre-smoothed u and
-    its post-smoothing pass recomputes it, k_xsmooth RE) is bitwise the
-    stored-u_pre schedule (xre 0)."""
-    kw = dict(kw)
-    tune = {k: kw.pop(k) for k in list(kw) if k in ("sep_velocity",)}
-    old = {k: _lib.get_tuning(k) for k in ("xre", *tune)}
-    out = {}
-    try:
-        for k, v in tune.items():
-            _lib.set_tuning(k, v)
-        for xr in (0, 1):
-            _lib.set_tuning("xre", xr)
-            if steps:
-                out[xr] = _steps(N, L, steps, _lib.FP_FMA, **kw)
-            else:
-                out[xr] = _cycles(N, L, 3, _lib.FP_FMA, **kw)
-    finally:
-        for k, v in old.items():
-            _lib.set_tuning(k, v)
-    assert np.array_equal(out[1][0], out[0][0])
-    assert out[1][1] == out[0][1]   # the level-0 pass is the same: norms bitwise
-
-
 def test_fma_mode_rejected_value():
     with pytest.raises(_lib.MGXError):
         Multigrid(64, 2, 1e-3, NU, fp_mode=7)
