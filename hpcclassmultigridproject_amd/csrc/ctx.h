@@ -184,6 +184,9 @@ extern long g_dist_min_rows;
 // tuning key "dist_overlap" (dist.hip): finest-level ghost exchange on a second
 // stream beside the interior of the cross-cycle pass
 extern long g_dist_overlap;
+// tuning key "dist_local_side" (dist.hip): virtual ranks' early exchanges on
+// the compute stream (0) or the second stream (1)
+extern long g_dist_local_side;
 // tuning key "cross_cycle" (mgx.hip); levels with n >= kCrossMinN can use it
 bool cross_cycle_on();
 constexpr long kCrossMinN = 4096;

@@ -52,6 +52,13 @@ long g_dist_min_rows = 256;
 // nothing of the local HBM -- bench.py prices 0 / 1 / 2 on the N-GPU run
 // itself and keeps the fastest for its timed region
 long g_dist_overlap = -1;
+// tuning key "dist_local_side": virtual ranks (one device) run the
+// dist_overlap exchanges at their early points ON the compute stream (0,
+// default: one chip has no second link to overlap with -- on a second stream
+// the copy kernels waited for CUs held by the level passes and each join
+// cost a bubble, +5 % per cycle at G = 8) or on the second stream as over
+// RCCL (1: exercises the fork / join logic on one GPU).  Bitwise the same.
+long g_dist_local_side = 0;
 
 // the partition / exchange plan (plan.h, host-only)
 using mgxplan::alloc_rows;
@@ -397,19 +404,23 @@ template <class F>
 static int side_exchange(mgx_ctx *c, const std::vector<XF> &xs, F &&post,
                          hipEvent_t ev_extra = nullptr) {
     Dist *d = c->dist;
-    HIPCHK(hipEventRecord(d->ev_fork, c->stream));
-    HIPCHK(hipStreamWaitEvent(d->xs, d->ev_fork, 0));
+    // (virtual ranks, dist_local_side 0: the same schedule on the compute stream)
+    hipStream_t st = d->local && !g_dist_local_side ? c->stream : d->xs;
+    if (st != c->stream) {
+        HIPCHK(hipEventRecord(d->ev_fork, c->stream));
+        HIPCHK(hipStreamWaitEvent(st, d->ev_fork, 0));
+    }
     const bool rec = c->prof == 1 || c->prof == 2;
     hipEvent_t e0 = rec ? take_event(c) : nullptr, e1 = rec ? take_event(c) : nullptr;
-    if (e0) HIPCHK(hipEventRecord(e0, d->xs));
-    CHK(exchange_rows(c, xs, d->xs));
+    if (e0) HIPCHK(hipEventRecord(e0, st));
+    CHK(exchange_rows(c, xs, st));
     if (e0 && e1) {
-        HIPCHK(hipEventRecord(e1, d->xs));
+        HIPCHK(hipEventRecord(e1, st));
         const double b = halo_bytes(c, xs);
         c->pending.push_back({MGX_K_HALO, 0, b, b, e0, e1});
     }
-    HIPCHK(hipEventRecord(d->ev_join, d->xs));
-    if (ev_extra) HIPCHK(hipEventRecord(ev_extra, d->xs));
+    HIPCHK(hipEventRecord(d->ev_join, st));
+    if (ev_extra) HIPCHK(hipEventRecord(ev_extra, st));
     d->early_pending = true;
     post();
     return MGX_OK;

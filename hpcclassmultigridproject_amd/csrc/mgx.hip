@@ -1358,6 +1358,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgxi::g_dist_overlap = value;
         return MGX_OK;
     }
+    if (!strcmp(key, "dist_local_side")) {
+        if (value != 0 && value != 1) return fail(MGX_E_ARG, "dist_local_side must be 0 or 1");
+        mgxi::g_dist_local_side = value;
+        return MGX_OK;
+    }
     if (!strcmp(key, "dist_min_rows")) {
         if (value < 16 || (value & 1)) return fail(MGX_E_ARG, "dist_min_rows must be even, >= 16");
         mgxi::g_dist_min_rows = value;
@@ -1453,6 +1458,10 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "dist_overlap")) {
         *value = mgxi::g_dist_overlap;
+        return MGX_OK;
+    }
+    if (!strcmp(key, "dist_local_side")) {
+        *value = mgxi::g_dist_local_side;
         return MGX_OK;
     }
     if (!strcmp(key, "dist_min_rows")) {

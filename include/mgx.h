@@ -194,6 +194,10 @@ int mgx_synchronize(mgx_ctx *ctx);
  * to the ghosts after it; 0 = every exchange on the compute stream; -1
  * (default) = 1 on an RCCL communicator, 0 on virtual ranks (one GPU, where
  * the side stream's copies compete with the passes).  Bitwise the same results.
+ * "dist_local_side": virtual ranks only: 0 (default) runs the dist_overlap
+ * exchanges at their early points on the compute stream (one device: no
+ * second link to overlap with), 1 on the second stream as over RCCL.  Bitwise
+ * the same results.
  * "xfast": 1 (default) runs the cross-cycle pass as an unguarded kernel over
  * the interior strips and rows plus a guarded kernel over the boundary strips
  * and bands; 0 = one guarded launch (bitwise the same results).

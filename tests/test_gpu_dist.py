@@ -310,13 +310,23 @@ def overlap():
     _lib.set_tuning("dist_overlap", old)
 
 
+@pytest.fixture(params=[0, 1], ids=["inline", "side_stream"])
+def local_side(request):
+    old = _lib.get_tuning("dist_local_side")
+    _lib.set_tuning("dist_local_side", request.param)
+    yield request.param
+    _lib.set_tuning("dist_local_side", old)
+
+
 @pytest.mark.parametrize("G", [2, 4, 8])
-def test_overlapped_exchange_bitwise(G, overlap):
+def test_overlapped_exchange_bitwise(G, overlap, local_side):
     """dist_overlap = 1 (finest ghost rows exchanged on a second stream behind
     the coarse levels) and 2 (plus the level-1 exchange beside the interior of
     the cross pass, the two ghost bands after it) give the same u bitwise as
     the serialised schedule and as one GPU, norms to the summation-order
-    tolerance (the split pass sums its partials in another order)."""
+    tolerance (the split pass sums its partials in another order); with the
+    virtual ranks' exchanges inline (dist_local_side 0) and on the second
+    stream (1: the RCCL transport's fork / join on one GPU)."""
     N, L = 4096, 7
     dt = 1.0 / N / 10
     us, ns, rs, _ = _run(N, L, dt, NU, 4)
