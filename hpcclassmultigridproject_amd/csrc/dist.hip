@@ -289,10 +289,11 @@ struct CopyBatch {
 struct PtrList {
     const double *p[kMaxCopies];
     int n;
+    int cont;   // continue the sum in *out (more than kMaxCopies parts)
 };
 __global__ void k_sum_list(const PtrList L, double *out) {
     if (threadIdx.x == 0) {
-        double t = 0.0;
+        double t = L.cont ? *out : 0.0;
         for (int i = 0; i < L.n; ++i) t += *L.p[i];
         *out = t;
     }
@@ -497,12 +498,15 @@ static int reduce_norm(mgx_ctx *c, double *norm) {
     double tot = 0.0;
     if (d->local) {
         PtrList pl{};
-        for (auto &p : d->parts) {
-            if (pl.n == kMaxCopies) return fail(MGX_E_INTERNAL, "too many virtual ranks");
-            pl.p[pl.n++] = p.dsum;
+        for (size_t i = 0; i < d->parts.size(); ++i) {
+            pl.p[pl.n++] = d->parts[i].dsum;
+            if (pl.n == kMaxCopies || i + 1 == d->parts.size()) {
+                hipLaunchKernelGGL(k_sum_list, dim3(1), dim3(64), 0, c->stream, pl, d->dsum_all);
+                HIPCHK(hipGetLastError());
+                pl.n = 0;
+                pl.cont = 1;
+            }
         }
-        hipLaunchKernelGGL(k_sum_list, dim3(1), dim3(64), 0, c->stream, pl, d->dsum_all);
-        HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(d->hsum, d->dsum_all, sizeof(double), hipMemcpyDeviceToHost,
                               c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));

@@ -213,7 +213,10 @@ __global__ __launch_bounds__(64 * WPB, (WCfg<K, MODE>::MINB)) void k_wsmooth(
 
         double2 ur[NR];
         RowData rd[NR];
-        constexpr bool WH = !C::RHSN;   // cn, cs stored per row
+#ifndef MGX_WH
+#define MGX_WH 1
+#endif
+        constexpr bool WH = MGX_WH && !C::RHSN;   // cn, cs stored per row
         CoefRow cf[NR];
 #pragma unroll
         for (int q = 0; q < NR; ++q) {

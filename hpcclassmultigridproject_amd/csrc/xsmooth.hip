@@ -117,7 +117,9 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     // pass is bound by loads in flight, not by VALU: rhs/v 2 -> 3 -> 4 steps
     // took level 0 -4 % and -3 % at the same VGPR count (B's path sets it);
     // u 3-4 steps or rhs/v 5 measured no better (N=16384, tools/ab_libs.sh).
-    constexpr int XRV = MGX_XRV;
+    // (the fma interior kernel on the velocity factors: 5 steps, -0.8 % on
+    // level 0 in three alternated rounds, 2 VGPRs spilled; XU 3 no change)
+    constexpr int XRV = (FM && SV && !G && !RS) ? MGX_XRV + 1 : MGX_XRV;
     constexpr int XU = MGX_XU;
     // A forms each row's coefficients once (MGX_XACOEF; B always does).  Not
     // in the guarded edge kernel: there it takes the kernel past 256 VGPRs
