@@ -78,6 +78,9 @@ struct WCfg {
 #ifndef MGX_WRV
 #define MGX_WRV 4
 #endif
+#ifndef MGX_WU
+#define MGX_WU 2
+#endif
 
 
 // G = false: the unguarded march (interior strips, rows [TOP, n+1-BOT) of
@@ -106,6 +109,9 @@ __global__ __launch_bounds__(64 * WPB, (WCfg<K, MODE>::MINB)) void k_wsmooth(
     // row's v two steps before its first stage
     constexpr int WRV = C::RHSN ? (MGX_WRV > 4 ? MGX_WRV : 4) : MGX_WRV;
     static_assert(WRV >= 2 && WRV <= NR - S + 1, "rhs/v prefetch distance");
+    // u rows (+ coarse parents) WU steps ahead of entering the u ring
+    constexpr int WU = MGX_WU < NR - 3 ? MGX_WU : NR - 3;
+    static_assert(WU >= 1 && WU <= NR - 3, "u prefetch distance");
     // WPB waves per workgroup march WPB adjacent strips over the same rows,
     // independently (no barriers); their row loads are adjacent 1-KiB pieces
     // of the same rows, issued at about the same time
@@ -140,8 +146,11 @@ __global__ __launch_bounds__(64 * WPB, (WCfg<K, MODE>::MINB)) void k_wsmooth(
             double2 X;
             double q00, q01, q10, q11;
         };
-        UPre up[2];
-        up[0] = up[1] = UPre{make_double2(0.0, 0.0), 0.0, 0.0, 0.0, 0.0};
+        // u rows (+ coarse parents) in flight, a ring by row like rd: row R in
+        // slot R mod NR, loaded WU steps before it enters the u ring
+        UPre up[NR];
+#pragma unroll
+        for (int q = 0; q < NR; ++q) up[q] = UPre{make_double2(0.0, 0.0), 0.0, 0.0, 0.0, 0.0};
         const int cl = min(max(c0, 0), (int)pitch - 2);
         const int jl = cl >> 1;
         const int j1 = (jl + 1 <= nc) ? 1 : 0;
@@ -251,11 +260,11 @@ __global__ __launch_bounds__(64 * WPB, (WCfg<K, MODE>::MINB)) void k_wsmooth(
         // flight (sets 1 / 0), rhs/v rows s+1, s+2 loaded
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-            load_u(s + d, up[0], d & 1);
-            ur[d] = make_u(s + d, up[0], d & 1);
+            load_u(s + d, up[d], d & 1);
+            ur[d] = make_u(s + d, up[d], d & 1);
         }
-        load_u(s + 3, up[1], true);
-        load_u(s + 4, up[0], false);
+#pragma unroll
+        for (int d = 3; d < 3 + WU; ++d) load_u(s + d, up[d % NR], d & 1);
 #pragma unroll
         for (int d = 1; d < WRV; ++d) load_rv(s + d, rd[d]);
         // RHSN: rhs of row r (ring slot iR) from its original u rows r-1..r+1,
@@ -304,8 +313,8 @@ __global__ __launch_bounds__(64 * WPB, (WCfg<K, MODE>::MINB)) void k_wsmooth(
 #pragma unroll
             for (int p = 0; p < NR; ++p) {
                 // (1) u row s+3 enters the ring; its prefetch set takes row s+5
-                ur[(p + 3) % NR] = make_u(s + 3, up[(p + 1) & 1], (p + 3) & 1);
-                load_u(s + 5, up[(p + 1) & 1], (p + 1) & 1);
+                ur[(p + 3) % NR] = make_u(s + 3, up[(p + 3) % NR], (p + 3) & 1);
+                load_u(s + 3 + WU, up[(p + 3 + WU) % NR], (p + 3 + WU) & 1);
                 // t of the row first used in this step: s+2 (RHSN), else s+1
                 scale_rv(rd[(p + (C::RHSN ? 2 : 1)) % NR]);
                 if (WH) {   // cn, cs of row s+1 from t1 (gs.cpp:128-129's cc, dd)
