@@ -144,10 +144,6 @@ bool xstep_supported(long n);
 // Cross pass: 1 = interior strips run the unguarded march (default), 0 = all guarded.
 void set_xfast(long v);
 long get_xfast();
-// Whole-level cross pass: CUs reserved for its edge launch beside the interior
-// one (CU-masked stream pair, multiple of 8; 0 = off)
-void set_xcu_edge(long v);
-long get_xcu_edge();
 void set_march_tile_rows(long v);
 long get_march_tile_rows();
 // Cross pass on row blocks of <= xtile_max_rows rows (default 4097): edges as

@@ -1368,12 +1368,6 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgxi::g_dist_min_rows = value;
         return MGX_OK;
     }
-    if (!strcmp(key, "xcu_edge")) {
-        if (value < 0 || value > 128 || value % 8)
-            return fail(MGX_E_ARG, "xcu_edge must be a multiple of 8 in [0, 128]");
-        mgx::set_xcu_edge(value);
-        return MGX_OK;
-    }
     if (!strcmp(key, "xfast")) {
         if (value != 0 && value != 1) return fail(MGX_E_ARG, "xfast must be 0 or 1");
         mgx::set_xfast(value);
@@ -1472,10 +1466,6 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "dist_min_rows")) {
         *value = mgxi::g_dist_min_rows;
-        return MGX_OK;
-    }
-    if (!strcmp(key, "xcu_edge")) {
-        *value = mgx::get_xcu_edge();
         return MGX_OK;
     }
     if (!strcmp(key, "xfast")) {

@@ -827,15 +827,13 @@ static int xsmooth_slots() {
 // partials written (grid * 2 * WPB: one per wave) at `partials`.
 template <int WPB, int K, bool G, bool RS, bool SV, bool FM>
 static int xsmooth_launch_sv(const XArgs &A, const MarchRegions &reg, double *partials, int lo,
-                             int hi, long min_rows, long max_wgs, hipStream_t s, double cu_frac = 1.0) {
+                             int hi, long min_rows, long max_wgs, hipStream_t s) {
     const long total = reg.pre[reg.count];
     if (total <= 0) return 0;
     long upw;
     MarchRegions r;
     using X = XCfg<K>;
-    // (cu_frac: the launch runs on that share of the CUs, a CU-masked stream)
-    const long slots = std::max(1L, (long)(xsmooth_slots<WPB, K, G, RS, SV, FM>() * cu_frac));
-    const unsigned grid = plan_march(reg, WPB, slots, min_rows,
+    const unsigned grid = plan_march(reg, WPB, xsmooth_slots<WPB, K, G, RS, SV, FM>(), min_rows,
                                      max_wgs, X::EA + X::EB + X::D + X::NR / 2, upw, r);
     // RS: the second partials (the next step's initial norm) at the same
     // offsets, kNormBlocks further on
@@ -849,80 +847,21 @@ static int xsmooth_launch_sv(const XArgs &A, const MarchRegions &reg, double *pa
 // level's fp_mode (Coef::fm)
 template <int WPB, int K, bool G, bool RS = false>
 static int xsmooth_launch(const XArgs &A, const MarchRegions &reg, double *partials, int lo, int hi,
-                          long min_rows, long max_wgs, hipStream_t s, double cu_frac = 1.0) {
+                          long min_rows, long max_wgs, hipStream_t s) {
     const bool sv = A.sa1 && A.sb1 && A.sa2 && A.sb2;
     if (A.c.fm) {
         if (sv)
             return xsmooth_launch_sv<WPB, K, G, RS, true, true>(A, reg, partials, lo, hi,
-                                                               min_rows, max_wgs, s, cu_frac);
+                                                               min_rows, max_wgs, s);
         return xsmooth_launch_sv<WPB, K, G, RS, false, true>(A, reg, partials, lo, hi, min_rows,
-                                                            max_wgs, s, cu_frac);
+                                                            max_wgs, s);
     }
     if (sv)
         return xsmooth_launch_sv<WPB, K, G, RS, true, false>(A, reg, partials, lo, hi, min_rows,
-                                                            max_wgs, s, cu_frac);
+                                                            max_wgs, s);
     return xsmooth_launch_sv<WPB, K, G, RS, false, false>(A, reg, partials, lo, hi, min_rows,
-                                                         max_wgs, s, cu_frac);
+                                                         max_wgs, s);
 }
-
-// tuning key "xcu_edge": CUs reserved for the edge launch, which then runs
-// BESIDE the interior launch on a CU-masked stream pair (0 = off: the edge
-// launch after the interior one on the context stream).  The interior march
-// is bound by the memory path, not by the CUs it occupies; the edge launch is
-// a latency-bound chain of row steps that the interior's CUs would otherwise
-// wait for.  Reserved CUs: bit 32a + 8b + ((a + t) mod 8) of the mask for
-// a = 0..7, b = 0..3, t = 0, 1, ... -- the same count on each of the 8 XCDs
-// whether the mask's bits run XCD-major or interleave over the XCDs.
-long g_xcu_edge = 0;
-void set_xcu_edge(long v) { g_xcu_edge = v; }
-long get_xcu_edge() { return g_xcu_edge; }
-namespace {
-struct CuSplit {
-    int dev = -1;
-    long reserved = 0;
-    int cus = 0;
-    hipStream_t si = nullptr, se = nullptr;   // interior / edge
-    hipEvent_t fork = nullptr, ji = nullptr, je = nullptr;
-};
-CuSplit g_cus;
-// the stream pair for `reserved` edge CUs on the current device (null on failure)
-CuSplit *cu_split(long reserved) {
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        return nullptr;
-    if (cus != 256 || reserved <= 0 || reserved % 8 || reserved >= cus) return nullptr;
-    CuSplit &c = g_cus;
-    if (c.dev == dev && c.reserved == reserved) return &c;
-    if (c.si) {
-        (void)hipStreamDestroy(c.si);
-        (void)hipStreamDestroy(c.se);
-        c.si = c.se = nullptr;
-    }
-    uint32_t me[8] = {0}, mi[8];
-    long n = 0;
-    for (int t = 0; t < 8 && n < reserved; ++t)
-        for (int b = 0; b < 4 && n < reserved; ++b)
-            for (int a = 0; a < 8; ++a, ++n) {
-                const int i = 32 * a + 8 * b + (a + t) % 8;
-                me[i >> 5] |= 1u << (i & 31);
-            }
-    for (int k = 0; k < 8; ++k) mi[k] = ~me[k];
-    if (hipExtStreamCreateWithCUMask(&c.si, 8, mi) != hipSuccess ||
-        hipExtStreamCreateWithCUMask(&c.se, 8, me) != hipSuccess)
-        return nullptr;
-    if (!c.fork) {
-        if (hipEventCreateWithFlags(&c.fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c.ji, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c.je, hipEventDisableTiming) != hipSuccess)
-            return nullptr;
-    }
-    c.dev = dev;
-    c.cus = cus;
-    c.reserved = reserved;
-    return &c;
-}
-}  // namespace
 
 static void add_tile_region(TileRegions &r, int c0, int c1, int r0, int r1, int TR) {
     if (c1 <= c0 || r1 <= r0) return;
@@ -1051,25 +990,6 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
     march_regions<WPB>(n, X::W, X::H, ra, rb, top, bot, split, inner, unused);
     march_regions<1>(n, X::W, X::H, ra, rb, top, bot, split, unused, edge);
     int pm = A.partials_done;
-    CuSplit *cs = (split && A.phase == 0 && g_xcu_edge > 0) ? cu_split(g_xcu_edge) : nullptr;
-    if (cs) {   // the two launches side by side on disjoint CUs
-        const double fe = (double)cs->reserved / cs->cus;
-        if (hipEventRecord(cs->fork, s) != hipSuccess ||
-            hipStreamWaitEvent(cs->si, cs->fork, 0) != hipSuccess ||
-            hipStreamWaitEvent(cs->se, cs->fork, 0) != hipSuccess)
-            return -4;
-        pm = xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, A.min_rows,
-                                           kNormBlocks / (2 * WPB) / 2, cs->si, 1.0 - fe);
-        const int pe = xsmooth_launch<1, K, true>(A, edge, A.partials + pm, lo, hi,
-                                                  std::min(MGX_XEDGE_ROWS, A.min_rows),
-                                                  kNormBlocks / 2 / 2, cs->se, fe);
-        if (hipEventRecord(cs->ji, cs->si) != hipSuccess ||
-            hipEventRecord(cs->je, cs->se) != hipSuccess ||
-            hipStreamWaitEvent(s, cs->ji, 0) != hipSuccess ||
-            hipStreamWaitEvent(s, cs->je, 0) != hipSuccess)
-            return -4;
-        return pm + pe;
-    }
     if (A.phase != 2)
         pm = xsmooth_launch<WPB, K, false>(A, inner, A.partials, lo, hi, A.min_rows,
                                            kNormBlocks / (2 * WPB) / 2, s);

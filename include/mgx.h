@@ -201,9 +201,6 @@ int mgx_synchronize(mgx_ctx *ctx);
  * "xfast": 1 (default) runs the cross-cycle pass as an unguarded kernel over
  * the interior strips and rows plus a guarded kernel over the boundary strips
  * and bands; 0 = one guarded launch (bitwise the same results).
- * "xcu_edge": CUs (a multiple of 8, <= 128) reserved for the cross pass's
- * edge launch, which then runs beside the interior launch on a CU-masked
- * stream pair (whole levels); 0 (default) = after it.  Bitwise the same.
  * "march_tile_rows": a row block whose wave march would give each resident
  * workgroup fewer than this many rows runs as LDS tiles (default 16, >= 0).
  * "xtile_max_rows": on row blocks of at most this many rows (a rank of a

@@ -288,23 +288,3 @@ def test_wcycle_cross_vs_oracle_and_partitioned(oracle_mod, cross):
         _lib.set_tuning("dist_min_rows", old)
     assert np.array_equal(outs[0], t.ufine)
     assert np.array_equal(outs[1], outs[0])
-
-
-@pytest.mark.parametrize("fp", [_lib.FP_BITWISE, _lib.FP_FMA], ids=["bitwise", "fma"])
-@pytest.mark.parametrize("N,L,kw", [(8192, 5, {}), (8192, 6, dict(nsmooth=2))],
-                         ids=["N8192", "N8192nu2"])
-def test_edge_beside_interior_on_masked_cus(N, L, kw, fp, cross):
-    """xcu_edge > 0: the edge launch runs beside the interior launch on a
-    CU-masked stream pair -- u and the cycle sequence bitwise the sequential
-    launches, norms to the summation order."""
-    old = _lib.get_tuning("xcu_edge")
-    out = {}
-    try:
-        for cu in (0, 32):
-            _lib.set_tuning("xcu_edge", cu)
-            out[cu] = _cycles(N, L, 3, 1, cross, fp_mode=fp, **kw)
-    finally:
-        _lib.set_tuning("xcu_edge", old)
-    assert out[32][2] == out[0][2] == 3
-    assert np.array_equal(out[32][0], out[0][0])
-    np.testing.assert_allclose(out[32][1], out[0][1], rtol=NORM_RTOL)
