@@ -66,6 +66,7 @@ using mgxplan::gather_rows;
 using mgxplan::ghost_plan;
 using mgxplan::kGhost;
 using mgxplan::kGhostFine;
+using mgxplan::kPostExt;
 using mgxplan::plan_rows;
 using mgxplan::Xfer;
 static int plan_la(long n0, int L, int world) {
@@ -540,12 +541,27 @@ static mgx::SmoothArgs args_for(const PLevel &L) {
     return A;
 }
 
+// Communication-avoiding post-smoothing: when a level's post-smoothing is ONE
+// pass (nsmooth <= fuse), a coarse level's post pass also computes the
+// kPostExt rows past each end of its block -- exactly what the neighbours
+// compute there (same inputs, same operations: bitwise), from its 16 ghost
+// rows of u_pre and rhs -- so the finer level's prolongation reads its own
+// copy and the corrected u is never exchanged: one RCCL group per coarse
+// level and cycle off the critical path (the u_pre ghosts before the pass
+// stay, on the side stream with dist_overlap).
+static bool post_ca(const mgx_ctx *c) {
+    const int fuse = std::max(1, std::min(c->opt.fuse, mgx::kSmoothMaxSweeps));
+    return c->opt.nsmooth >= 1 && c->opt.nsmooth <= fuse &&
+           kPostExt + 2 * c->opt.nsmooth <= mgxplan::kGhost;
+}
+
 // nsmooth sweeps on partitioned level l in passes of <= fuse sweeps; the
 // first pass may add the prolongation, the last may restrict or take the norm.
 static int smooth(mgx_ctx *c, int l, bool prolong, bool restrict_, bool norm) {
     Dist *d = c->dist;
     const int sweeps = c->opt.nsmooth;
     const int fuse = std::max(1, std::min(c->opt.fuse, mgx::kSmoothMaxSweeps));
+    const bool ca = post_ca(c);
     bool fresh = false;   // u ghosts exchanged early (dist_overlap)
     CHK(take_fresh(c, l, &fresh));
     for (int done = 0; done < sweeps;) {
@@ -556,7 +572,9 @@ static int smooth(mgx_ctx *c, int l, bool prolong, bool restrict_, bool norm) {
         const bool rs = restrict_ && last;
         const bool nm = norm && last && !rs;
         const bool ufresh = fresh && first;
-        if (!zero && pr && l + 1 < d->la)
+        // (the coarser level's u for the prolongation: its own rows past the
+        // block, ca, or its ghost rows exchanged)
+        if (!zero && pr && l + 1 < d->la && !ca)
             CHK(ufresh ? xchg(c, l + 1, kU) : xchg(c, {XF{l, kU}, XF{l + 1, kU}}));
         else if (!zero && !ufresh)
             CHK(xchg(c, l, kU));
@@ -568,6 +586,10 @@ static int smooth(mgx_ctx *c, int l, bool prolong, bool restrict_, bool norm) {
         for (auto &p : d->parts) {
             PLevel &L = p.lv[l];
             mgx::SmoothArgs A = args_for(L);
+            if (pr && ca && l >= 1) {   // + kPostExt rows past each end
+                A.ra = std::max(0, L.ra - kPostExt);
+                A.rb = (int)std::min<long>(L.n + 1, (long)L.rb + kPostExt);
+            }
             if (pr || rs) {
                 if (l + 1 < d->la) {
                     PLevel &Cl = p.lv[l + 1];
@@ -675,7 +697,7 @@ static int dist_cross(mgx_ctx *c, bool store_post) {
     CHK(take_fresh(c, 0, &fresh));
     std::vector<XF> xl;
     if (!fresh) xl.push_back(XF{0, kU});
-    if (1 < d->la) xl.push_back(XF{1, kU});
+    if (1 < d->la && !post_ca(c)) xl.push_back(XF{1, kU});
     // (the split launches are the unguarded kernel's: xfast on, d > 0)
     bool ov = overlap_mode(d) == 2 && d->world > 1 && !xl.empty() && mgx::get_xfast() != 0;
     for (auto &p : d->parts) ov = ov && p.lv[0].rb - p.lv[0].ra >= 4 * G && p.lv[0].coef.dgs > 0;

@@ -6,9 +6,11 @@
 //
 // Levels 0..la-1 are split into contiguous row blocks, one per rank, with
 // boundaries at even rows (restriction rows 2I and prolongation parents stay
-// local); each block also holds ghost rows of its neighbours: kGhostFine on
-// level 0 (the cross-cycle pass's cone is 14 rows), kGhost elsewhere (a fused
-// K<=3 pass + residual has a cone of E <= 7 rows).
+// local); each block also holds kGhost = 16 ghost rows of its neighbours on
+// every level: the cross-cycle pass's cone on level 0 is 14 rows, and on the
+// coarser levels a post-smoothing pass computes kPostExt rows past its block
+// as well (communication-avoiding: the finer level's prolongation then needs
+// no exchange of the corrected u), a cone of kPostExt + 2K <= 16 rows.
 #pragma once
 #include <algorithm>
 #include <string>
@@ -16,8 +18,14 @@
 
 namespace mgxplan {
 
-constexpr int kGhost = 8;        // >= the widest fused-pass cone (E <= 7) + 1
+constexpr int kGhost = 16;       // >= the widest cone (see above)
 constexpr int kGhostFine = 16;   // level 0: the cross-cycle pass's cone is 14 rows
+// Rows past its block (each side) a coarse level's post-smoothing pass
+// computes: the finer level's pass with a cone of c rows (its output + its
+// stages) reads coarse rows ra/2 - c/2 .. rb/2 + c/2 (the odd row's second
+// parent): c = 14 for the cross pass, kPostExt + 2K <= 16 for a coarse post
+// pass, so 10 rows (even: row blocks start at even rows) cover every level.
+constexpr int kPostExt = 10;
 
 // Rows [ra, rb) of level l owned by `rank` (the same rule on every rank; the
 // last rank also owns the boundary row n).

@@ -16,7 +16,11 @@ here exchange exactly the rows, offsets and counts the RCCL ranks do; a rank's
 allocated rows are what that plan receives, everything else is NaN.
 
 Mirrors: dist.hip dist_level (pre pass + restrict, recurse / gather, post
-pass + prolong), multigrid.cpp:17-92 for the replicated levels.
+pass + prolong), multigrid.cpp:17-92 for the replicated levels.  Post passes
+are communication-avoiding (dist.hip post_ca): a coarse level's corrected u
+is NOT exchanged; only its rows within POST_EXT of its block (which its own
+post pass computed) are kept, every other row is poisoned before the finer
+level prolongs from it.
 """
 from __future__ import annotations
 
@@ -28,7 +32,8 @@ import torch.distributed as dist
 
 from oracle import oracle as O
 
-K_GHOST = 8         # dist.hip kGhost (the fewest ghost rows a block may hold)
+K_GHOST = 16        # plan.h kGhost (the fewest ghost rows a block may hold)
+POST_EXT = 10       # plan.h kPostExt: rows past its block a coarse post pass computes
 
 
 class Block:
@@ -143,8 +148,7 @@ class PartitionedVCycle:
         # post-smoothing pass: prolongation + add, sweeps (+ residual norm)
         exchange(b, self.u[l], self.rank, self.world)
         if l + 1 < self.la:
-            exchange(self.blk[l + 1], self.u[l + 1], self.rank, self.world)
-            self.blk[l + 1].poison(self.u[l + 1])
+            self._keep_post_rows(l + 1)
         b.poison(self.u[l])
         self.u[l] += O.prolongation(self.u[l + 1], nc)
         self._gs(l)
@@ -155,6 +159,14 @@ class PartitionedVCycle:
             dist.all_reduce(part)
             return math.sqrt(float(part[0]))
         return None
+
+    def _keep_post_rows(self, l):
+        """Level l's u after its post pass: valid on its block +- POST_EXT rows
+        only (no exchange); poison the rest."""
+        b = self.blk[l]
+        m = b.rows(self.u[l])
+        m[: max(0, b.ra - POST_EXT)] = np.nan
+        m[b.rb + POST_EXT:] = np.nan
 
     def _gather_rhs(self, l):
         """dist.hip gather_rhs: the in-place all-gather of mgx_gather_plan's rows."""
@@ -205,8 +217,7 @@ class PartitionedVCycle:
         self._coarse_cycle(1)
         exchange(b, self.u[0], self.rank, self.world)
         if 1 < self.la:
-            exchange(self.blk[1], self.u[1], self.rank, self.world)
-            self.blk[1].poison(self.u[1])
+            self._keep_post_rows(1)
         b.poison(self.u[0])
         b.poison(self.rhs[0])
         self.u[0] += O.prolongation(self.u[1], n // 2)

@@ -76,34 +76,28 @@ def _assert_call_counts(v):
       rhs: u ghosts before, rhs ghosts after -> 2 groups, 2 nb sends;
       plain V-cycle (dist_level, mg_inner and cycles without the cross pass):
         level 0 pre (u) + coarse rhs of level 1, the restricted rhs of levels
-        2..la-1, the all-gather into level la, the post pass of level la-1 (its
-        u) and of levels la-2..0 (u of the level and of the one below, one
-        group) -> 2 la groups, (3 la - 1) nb sends, 1 all-gather;
+        2..la-1, the all-gather into level la, the post pass of every level
+        (its own u_pre ghosts only: the coarser level's corrected u is never
+        exchanged, dist.hip post_ca) -> 2 la groups, 2 la nb sends, 1
+        all-gather;
       a cycle with the cross pass, from the state the last one left (the
         second run_cycles(1)): no level-0 pre pass; the cross pass exchanges
-        the level-0 and level-1 u in one group and then the level-1 rhs ->
-        2 la - 1 groups, (3 la - 2) nb sends;
+        the level-0 u and then the level-1 rhs -> 2 la - 1 groups, (2 la - 1)
+        nb sends;
       + 1 all-reduce per cycle that takes a norm.
     dist_overlap >= 1 (early_u): every partitioned level's pre-smoothed u
     ghosts go as a group of their own on the side stream right after its
-    pre pass, and the level's post pass exchanges only the coarser level's u
-    (level la-1's post pass none): the same sends in la - 1 more groups (V-cycle)
-    / la - 1 more (cross cycle: levels 1..la-1 and the level-0 u after the
-    cross pass, minus level la-1's post group).
+    pre pass instead of before its post pass: the same counts.
     Receives equal sends; no broadcast outside the download."""
     sc = v["scenario"]
     la, G = v["replicated_level"], sc["world"]
-    ov = sc.get("overlap", 0)
-    if ov < 0:
-        ov = 1   # the default on an RCCL communicator
     cross = sc["N"] >= 4096
     for r, ph in enumerate(v["phase_calls"]):
         nb = 1 if r in (0, G - 1) else 2
-        early = la - 1 if ov >= 1 else 0
         exp = {"rhs": (2, 2 * nb, 0, 0),
-               "vcycle": (2 * la + early, (3 * la - 1) * nb, 1, 0),
-               "cycle1": ((2 * la - 1 + early, (3 * la - 2) * nb, 1, 1) if cross
-                          else (2 * la + early, (3 * la - 1) * nb, 1, 1))}
+               "vcycle": (2 * la, 2 * la * nb, 1, 0),
+               "cycle1": ((2 * la - 1, (2 * la - 1) * nb, 1, 1) if cross
+                          else (2 * la, 2 * la * nb, 1, 1))}
         for phase, (groups, sends, gathers, reduces) in exp.items():
             c = ph[phase]
             got = (c["ncclGroupStart"], c["ncclSend"], c["ncclAllGather"], c["ncclAllReduce"])
