@@ -51,7 +51,6 @@ struct Level {
     // rows < vz of v1 / v2 match the reference-tower generator (mgx::VGen)
     // from the finest level's factors (checked at upload)
     bool vgen = false;
-    double *vtab = nullptr;   // its column tables (VGen::bt1, bt2)
     mgx::Coef coef{};
     double M() const { return double(n + 1) * double(n + 1); }
     // compulsory bytes of v1 + v2 of this level (the zero rows cost no HBM)
@@ -149,7 +148,7 @@ int build_tower(mgx_ctx *c);
 int find_zero_rows(mgx_ctx *c);
 // Level::vgen of levels 1..3 (reference tower, finest factors present): their
 // rows [0, vz) checked equal to the generator's values (tuning key "vgen")
-int find_vgen_levels(mgx_ctx *c, const std::vector<double> &b1, const std::vector<double> &b2);
+int find_vgen_levels(mgx_ctx *c);
 extern long g_vgen;
 // velocity factors of level 0 from host copies of v1 / v2 (rows [r0, r0+rows)
 // of width n+1); false: not separable (or "sep_velocity" off), nothing set

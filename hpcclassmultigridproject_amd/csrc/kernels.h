@@ -79,15 +79,10 @@ constexpr int kModeRhsNorm = 16;
 // REFERENCE) regenerated from the finest level's rank-1 factors: level l's
 // (i, j) is next_l[i*(n_l+1) + j] with next_l[I*W + J] = next_{l-1}[2I*(2W-1)
 // + 2J] for I, J < W = N/4+1 (zero past W^2) and next_0 = the finest field
-// read flat, v0[r*(N+1) + c] = fl(a[r] * b[c]).  On levels 1 and 2 that is
-//   v(i, j) = a[2^l i + q] * b[2^l j - q(2W-1)],  q = floor(2^(l-1)(j-i)/W)
-// in {-1, 0, 1}, zero where the flat index i(2W-1)+j (l = 1) or i(N+2)+2j
-// (l = 2) reaches W^2 -- the stored value, bitwise (stencil.h vgen_pair,
-// tests/test_vgen_formula.py).  bt1 / bt2: per field the three column tables
-// bt[(q+1)(n_l+1) + j] = b[2^l j - q(2W-1)] (0 out of range); a1 / a2: the
-// finest row factors.  bt1 null: not used.
+// read flat, v0[r*(N+1) + c] = fl(a[r] * b[c]) -- the stored value, bitwise.
+// a1..b2 null: not used.
 struct VGen {
-    const double *bt1 = nullptr, *bt2 = nullptr, *a1 = nullptr, *a2 = nullptr;
+    const double *a1 = nullptr, *b1 = nullptr, *a2 = nullptr, *b2 = nullptr;
     int N = 0, W = 0, l = 0;
 };
 // 1 if level l's stored v1 / v2 rows [0, vz) equal the generator's values

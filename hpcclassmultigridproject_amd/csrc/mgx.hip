@@ -44,11 +44,10 @@ bool factor_velocity(const double *v1, const double *v2, long n, long r0, long r
 }
 
 void free_level_factors(Level &L) {
-    for (double **p : {&L.sa1, &L.sb1, &L.sa2, &L.sb2, &L.vtab}) {
+    for (double **p : {&L.sa1, &L.sb1, &L.sa2, &L.sb2}) {
         (void)hipFree(*p);
         *p = nullptr;
     }
-    L.vgen = false;
 }
 
 // Device copies: row factors at rows [row0, row0 + a.size()) of an (n+1)-row
@@ -710,50 +709,29 @@ long g_vgen = 0;
 
 static mgx::VGen level_vgen(const mgx_ctx *c, int l) {
     mgx::VGen g;
-    const Level &F = c->lv[0], &L = c->lv[l];
-    const long w = L.n + 1;
-    g.bt1 = L.vtab;
-    g.bt2 = L.vtab ? L.vtab + 3 * w : nullptr;
+    const Level &F = c->lv[0];
     g.a1 = F.sa1;
+    g.b1 = F.sb1;
     g.a2 = F.sa2;
+    g.b2 = F.sb2;
     g.N = (int)c->N;
     g.W = (int)(c->N / 4 + 1);
     g.l = l;
     return g;
 }
 
-// Levels 1 and 2 whose rows [0, vz) equal the generator's values bitwise
-// (reference tower, finest factors b1 / b2 given): their column tables
-// (VGen) uploaded, Level::vgen set.
-int find_vgen_levels(mgx_ctx *c, const std::vector<double> &b1, const std::vector<double> &b2) {
-    for (size_t l = 1; l < c->lv.size(); ++l) {
-        (void)hipFree(c->lv[l].vtab);
-        c->lv[l].vtab = nullptr;
-        c->lv[l].vgen = false;
-    }
+// Levels 1..3 whose rows [0, vz) equal the generator's values bitwise
+// (reference tower, finest factors present): Level::vgen.
+int find_vgen_levels(mgx_ctx *c) {
+    for (auto &L : c->lv) L.vgen = false;
     const Level &F = c->lv[0];
-    const long N = c->N;
-    if (c->opt.tower_mode != MGX_TOWER_REFERENCE || !F.sa1 || c->L < 2 || (N & 3) ||
-        N > 32768 || (long)b1.size() < N + 1 || (long)b2.size() < N + 1)
+    if (c->opt.tower_mode != MGX_TOWER_REFERENCE || !F.sa1 || c->L < 2 || (c->N & 3) ||
+        c->N > 32768)
         return MGX_OK;
-    const int top = std::min(c->L - 1, 2);
-    const long W = N / 4 + 1;
-    for (int l = 1; l <= top; ++l) {   // bt[f][(q+1)(n+1) + j] = b_f[2^l j - q(2W-1)]
-        Level &L = c->lv[l];
-        const long w = L.n + 1;
-        std::vector<double> t(6 * w, 0.0);
-        for (int f = 0; f < 2; ++f)
-            for (int q = -1; q <= 1; ++q)
-                for (long j = 0; j < w; ++j) {
-                    const long k = (j << l) - q * (2 * W - 1);
-                    if (k >= 0 && k <= N) t[(3 * f + q + 1) * w + j] = (f ? b2 : b1)[k];
-                }
-        HIPCHK(hipMalloc(&L.vtab, sizeof(double) * t.size()));
-        HIPCHK(hipMemcpy(L.vtab, t.data(), sizeof(double) * t.size(), hipMemcpyHostToDevice));
-    }
     int *dok = nullptr;
     HIPCHK(hipMalloc(&dok, sizeof(int) * 4));
     int rc = MGX_OK;
+    const int top = std::min(c->L - 1, 3);
     std::vector<int> ones(top + 1, 1), h(top + 1, 0);
     if (hipMemcpyAsync(dok, ones.data(), sizeof(int) * (top + 1), hipMemcpyHostToDevice,
                        c->stream) != hipSuccess)
@@ -1009,7 +987,7 @@ int mgxi::upload_ctx(mgx_ctx *c, const double *u0, const double *v1, const doubl
     if (kind == hipMemcpyHostToDevice && c->L > 1 && c->N >= kCrossMinN &&
         factor_velocity(v1, v2, c->N, 0, c->N + 1, L.coef.h * 0.5, a1, b1, a2, b2))
         CHK(set_level_factors(L, 0, a1, b1, a2, b2, c->stream));
-    CHK(find_vgen_levels(c, b1, b2));
+    CHK(find_vgen_levels(c));
     HIPCHK(hipStreamSynchronize(c->stream));
     return MGX_OK;
 }

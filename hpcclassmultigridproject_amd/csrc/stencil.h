@@ -187,22 +187,41 @@ constexpr int kFinalThreads = 1024;
 //
 // Work split (marches): a 1-D grid of workgroups, each with a share of the
 // (strip, row) space (MarchRegions below), so one launch is one balanced wave.
-// The reference tower's velocity at (i, j) of level l = 1, 2 (VGen,
-// kernels.h): the stored value, bitwise.  r: the row's factor index 2^l i.
-__device__ __forceinline__ void vgen_pair(const VGen &g, int i, int j, int nl, double &x,
-                                          double &y) {
-    const int W = g.W;
-    const long m = g.l == 1 ? (long)i * (2 * W - 1) + j : (long)i * (g.N + 2) + 2 * j;
-    if (j > nl || m >= (long)W * W) {
+// The reference tower's level-l entry (i, j) (VGen, kernels.h) as the finest
+// field's (r, c), or r = -1 where the tower holds zero.  Each of the l
+// injection steps maps next_s[m] (m < W^2) to next_{s-1}[I(N+2) + 2J], I, J =
+// divmod(m, W) (2(2W-1) = N+2); the last lands on the finest field read
+// flat, whose (r, c) is (I, I + 2J) -- I + 2J < 3W - 2 < N + 1, so no carry.
+// m < W^2 < 2^24: the quotient from an fp32 reciprocal, corrected by one.
+__device__ __forceinline__ void vgen_rc(const VGen &g, int i, int j, int nl, int &r, int &c) {
+    r = -1;
+    c = 0;
+    if (j > nl) return;
+    const int W = g.W, W2 = W * W, np2 = g.N + 2;
+    const float rw = 1.0f / (float)W;
+    int m = i * (nl + 1) + j;
+    for (int s = 0; s < g.l; ++s) {
+        if (m >= W2) return;
+        int I = (int)((float)m * rw);
+        I -= (I * W > m) ? 1 : 0;
+        I += ((I + 1) * W <= m) ? 1 : 0;
+        const int J = m - I * W;
+        if (s + 1 == g.l) {
+            r = I;
+            c = I + 2 * J;
+            return;
+        }
+        m = I * np2 + 2 * J;
+    }
+}
+// v1 and v2 of the entry: fl(a[r] * b[c]) -- the stored bits
+__device__ __forceinline__ void vgen_value(const VGen &g, int r, int c, double &x, double &y) {
+    if (r < 0) {
         x = y = 0.0;
         return;
     }
-    const int d = (j - i) << (g.l - 1);
-    const int q = d < 0 ? -1 : (d >= W ? 1 : 0);
-    const int r = (i << g.l) + q;
-    const long t = (long)(q + 1) * (nl + 1) + j;
-    x = g.a1[r] * g.bt1[t];
-    y = g.a2[r] * g.bt2[t];
+    x = g.a1[r] * g.b1[c];
+    y = g.a2[r] * g.b2[c];
 }
 
 struct RowData {

@@ -210,8 +210,11 @@ __global__ __launch_bounds__(64 * WPB, (WCfg<K, MODE>::MINB)) void k_wsmooth(
             const bool z = Rc >= vz;
             if (VG && !z) {
                 double x0, y0, x1, y1;
-                vgen_pair(vg, Rc, cl, n, x0, y0);
-                vgen_pair(vg, Rc, cl + 1, n, x1, y1);
+                int r0, k0, r1, k1;
+                vgen_rc(vg, Rc, cl, n, r0, k0);
+                vgen_rc(vg, Rc, cl + 1, n, r1, k1);
+                vgen_value(vg, r0, k0, x0, y0);
+                vgen_value(vg, r1, k1, x1, y1);
                 d.x = make_double2(x0, x1);
                 d.y = make_double2(y0, y1);
             } else {
@@ -697,7 +700,7 @@ static int wsmooth_launch(const SmoothArgs &A, const MarchRegions &reg, double *
     // (fp_mode fma: no division)
     // the reference tower's velocity generator on the V-cycle's coarse passes
     constexpr bool VGM = (MODE == 2 || MODE == 5) && G;
-    if (VGM && A.vg.bt1 && A.zrow) {
+    if (VGM && A.vg.a1 && A.zrow) {
         if (A.c.fm)
             return wsmooth_launch_pd<WPB, K, MODE, G, false, true, VGM>(A, reg, partials, max_wgs, s);
         if (A.c.dgs > 0)

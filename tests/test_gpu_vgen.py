@@ -47,7 +47,7 @@ def _run(N, L, vgen, cycles=3, steps=0, **kw):
 def test_generated_velocity_equals_stored(N, L, kw, steps):
     u1, o1, f1 = _run(N, L, 1, steps=steps, **kw)
     u0, o0, f0 = _run(N, L, 0, steps=steps, **kw)
-    assert f1 & 1 and f1 >> 1 & 1 and f1 < 8, f1   # finest factored, levels 1(-2) generated
+    assert f1 & 1 and f1 >> 1 & 1, f1            # finest factored, level 1 generated
     assert f0 == 1
     assert np.array_equal(u1, u0)
     assert o1 == o0
