@@ -679,9 +679,7 @@ __global__ __launch_bounds__(256) void k_vgen_check(const double *__restrict__ v
     const int i = blockIdx.y;
     for (int j = blockIdx.x * 256 + threadIdx.x; j <= n; j += gridDim.x * 256) {
         double x, y;
-        int r, c;
-        vgen_rc(g, i, j, n, r, c);
-        vgen_value(g, r, c, x, y);
+        vgen_value(g, vgen_index(g, i, j, n), x, y);
         const long o = (long)i * pitch + j;
         if (__double_as_longlong(x) != __double_as_longlong(v1[o]) ||
             __double_as_longlong(y) != __double_as_longlong(v2[o]))

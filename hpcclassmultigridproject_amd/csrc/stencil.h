@@ -187,41 +187,30 @@ constexpr int kFinalThreads = 1024;
 //
 // Work split (marches): a 1-D grid of workgroups, each with a share of the
 // (strip, row) space (MarchRegions below), so one launch is one balanced wave.
-// The reference tower's level-l entry (i, j) (VGen, kernels.h) as the finest
-// field's (r, c), or r = -1 where the tower holds zero.  Each of the l
-// injection steps maps next_s[m] (m < W^2) to next_{s-1}[I(N+2) + 2J], I, J =
-// divmod(m, W) (2(2W-1) = N+2); the last lands on the finest field read
-// flat, whose (r, c) is (I, I + 2J) -- I + 2J < 3W - 2 < N + 1, so no carry.
-// m < W^2 < 2^24: the quotient from an fp32 reciprocal, corrected by one.
-__device__ __forceinline__ void vgen_rc(const VGen &g, int i, int j, int nl, int &r, int &c) {
-    r = -1;
-    c = 0;
-    if (j > nl) return;
-    const int W = g.W, W2 = W * W, np2 = g.N + 2;
-    const float rw = 1.0f / (float)W;
-    int m = i * (nl + 1) + j;
+// Level-0 flat index of the reference tower's level-l entry (i, j) (VGen,
+// kernels.h), or -1 where the tower holds zero.  l <= 3 steps of the
+// injection, 32-bit (every index < (N+1)^2 < 2^31 for N <= 32768).
+__device__ __forceinline__ int vgen_index(const VGen &g, int i, int j, int nl) {
+    if (j > nl) return -1;
+    const unsigned W = (unsigned)g.W, W2 = W * W, sp = 2u * W - 1u;
+    unsigned m = (unsigned)i * (unsigned)(nl + 1) + (unsigned)j;
     for (int s = 0; s < g.l; ++s) {
-        if (m >= W2) return;
-        int I = (int)((float)m * rw);
-        I -= (I * W > m) ? 1 : 0;
-        I += ((I + 1) * W <= m) ? 1 : 0;
-        const int J = m - I * W;
-        if (s + 1 == g.l) {
-            r = I;
-            c = I + 2 * J;
-            return;
-        }
-        m = I * np2 + 2 * J;
+        if (m >= W2) return -1;
+        const unsigned I = m / W, J = m - I * W;
+        m = 2u * I * sp + 2u * J;
     }
+    return (int)m;
 }
-// v1 and v2 of the entry: fl(a[r] * b[c]) -- the stored bits
-__device__ __forceinline__ void vgen_value(const VGen &g, int r, int c, double &x, double &y) {
-    if (r < 0) {
+// v1 and v2 of the entry: fl(a[r] * b[c]), r, c = divmod(k, N+1)
+__device__ __forceinline__ void vgen_value(const VGen &g, int k, double &x, double &y) {
+    if (k < 0) {
         x = y = 0.0;
         return;
     }
-    x = g.a1[r] * g.b1[c];
-    y = g.a2[r] * g.b2[c];
+    const unsigned np = (unsigned)g.N + 1u;
+    const unsigned r = (unsigned)k / np, cc = (unsigned)k - r * np;
+    x = g.a1[r] * g.b1[cc];
+    y = g.a2[r] * g.b2[cc];
 }
 
 struct RowData {

@@ -210,11 +210,8 @@ __global__ __launch_bounds__(64 * WPB, (WCfg<K, MODE>::MINB)) void k_wsmooth(
             const bool z = Rc >= vz;
             if (VG && !z) {
                 double x0, y0, x1, y1;
-                int r0, k0, r1, k1;
-                vgen_rc(vg, Rc, cl, n, r0, k0);
-                vgen_rc(vg, Rc, cl + 1, n, r1, k1);
-                vgen_value(vg, r0, k0, x0, y0);
-                vgen_value(vg, r1, k1, x1, y1);
+                vgen_value(vg, vgen_index(vg, Rc, cl, n), x0, y0);
+                vgen_value(vg, vgen_index(vg, Rc, cl + 1, n), x1, y1);
                 d.x = make_double2(x0, x1);
                 d.y = make_double2(y0, y1);
             } else {
