@@ -604,13 +604,9 @@ def main():
                    "last_residual": res},
         "roofline": roof,
         "kernels": kernels,
-        "velocity": (("level 0: exact rank-1 factors (sep_velocity); coarse levels: all-zero "
-                      "rows from one L2-resident row (zero_rows)" +
-                      (", the other rows of levels " +
-                       ", ".join(str(l) for l in range(1, 4) if fac.value >> l & 1) +
-                       " regenerated from the level-0 factors (vgen: the reference tower's "
-                       "re-read of the rank-1 field, checked at upload)"
-                       if fac.value & ~1 else "")) if fac.value else "2-D arrays"),
+        "velocity": ("level 0: exact rank-1 factors (sep_velocity); coarse levels: all-zero "
+                     "rows from one L2-resident row (zero_rows)" if fac.value else
+                     "2-D arrays"),
         "other_fp_mode": other,
         "generic_velocity_path": generic,
     }

@@ -48,9 +48,6 @@ struct Level {
     // rows >= vz of v1 and v2 are all zeros (found at upload): the row march
     // reads them from mgx_ctx::zrow (L2-resident) instead of HBM
     int vz = 0x7fffffff;
-    // rows < vz of v1 / v2 match the reference-tower generator (mgx::VGen)
-    // from the finest level's factors (checked at upload)
-    bool vgen = false;
     mgx::Coef coef{};
     double M() const { return double(n + 1) * double(n + 1); }
     // compulsory bytes of v1 + v2 of this level (the zero rows cost no HBM)
@@ -146,10 +143,6 @@ int build_tower(mgx_ctx *c);
 // Level::vz of levels 1..L-1 from the built tower (the first row from which
 // every row of v1 and v2 is zero)
 int find_zero_rows(mgx_ctx *c);
-// Level::vgen of levels 1..3 (reference tower, finest factors present): their
-// rows [0, vz) checked equal to the generator's values (tuning key "vgen")
-int find_vgen_levels(mgx_ctx *c);
-extern long g_vgen;
 // velocity factors of level 0 from host copies of v1 / v2 (rows [r0, r0+rows)
 // of width n+1); false: not separable (or "sep_velocity" off), nothing set
 bool factor_velocity(const double *v1, const double *v2, long n, long r0, long rows, double smin,

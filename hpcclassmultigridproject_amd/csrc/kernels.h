@@ -75,20 +75,6 @@ enum : int { kModeZero = 1, kModeProlong = 2, kModeRestrict = 4, kModeNorm = 8 }
 // and the residual norm of uin against it goes to *norm_out -- a time step's
 // compute_rhs, mg_outer's initial norm and the first pre-smoothing in one pass.
 constexpr int kModeRhsNorm = 16;
-// The reference tower's coarse velocity (mgx.hip build_tower
-// REFERENCE) regenerated from the finest level's rank-1 factors: level l's
-// (i, j) is next_l[i*(n_l+1) + j] with next_l[I*W + J] = next_{l-1}[2I*(2W-1)
-// + 2J] for I, J < W = N/4+1 (zero past W^2) and next_0 = the finest field
-// read flat, v0[r*(N+1) + c] = fl(a[r] * b[c]) -- the stored value, bitwise.
-// a1..b2 null: not used.
-struct VGen {
-    const double *a1 = nullptr, *b1 = nullptr, *a2 = nullptr, *b2 = nullptr;
-    int N = 0, W = 0, l = 0;
-};
-// 1 if level l's stored v1 / v2 rows [0, vz) equal the generator's values
-// (checked on the device at upload), written to *ok (device int, preset 1)
-void launch_vgen_check(const double *v1, const double *v2, long n, long pitch, int vz, VGen g,
-                       int *ok, hipStream_t s);
 struct SmoothArgs {
     const double *uin;
     double *uout;
@@ -106,8 +92,6 @@ struct SmoothArgs {
     // from zrow (one zero row of >= pitch doubles, L2-resident) instead of HBM
     const double *zrow = nullptr;
     int vz = 0x7fffffff;
-    // rows < vz of v1 / v2 from the reference-tower generator (a1 set), not HBM
-    VGen vg{};
     bool norm_sqrt = true;
     bool norm_accumulate = false;   // NORM: add the plain sum to *norm_out
     // Row-block partitions (multi-GPU): output rows [ra, rb) and rows [lo, hi]

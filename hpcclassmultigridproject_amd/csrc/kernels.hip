@@ -671,31 +671,6 @@ void launch_injection_rows(double *dst, long dst_pitch, const double *src, long 
     MGX_LAUNCH(k_injection_rows, g, dim3(256), s, dst, dst_pitch, src, src_pitch, rows, cols);
 }
 
-namespace {
-// every entry (i < vz, j <= n) of v1 / v2 bitwise the generator's (VGen)
-__global__ __launch_bounds__(256) void k_vgen_check(const double *__restrict__ v1,
-                                                    const double *__restrict__ v2, int n, long pitch,
-                                                    VGen g, int *ok) {
-    const int i = blockIdx.y;
-    for (int j = blockIdx.x * 256 + threadIdx.x; j <= n; j += gridDim.x * 256) {
-        double x, y;
-        vgen_value(g, vgen_index(g, i, j, n), x, y);
-        const long o = (long)i * pitch + j;
-        if (__double_as_longlong(x) != __double_as_longlong(v1[o]) ||
-            __double_as_longlong(y) != __double_as_longlong(v2[o]))
-            atomicAnd(ok, 0);
-    }
-}
-}  // namespace
-
-void launch_vgen_check(const double *v1, const double *v2, long n, long pitch, int vz, VGen g,
-                       int *ok, hipStream_t s) {
-    const long rows = std::min<long>(vz, n + 1);
-    if (rows <= 0) return;
-    MGX_LAUNCH(k_vgen_check, dim3(cdiv(n + 1, 256 * 8), (unsigned)rows), dim3(256), s, v1, v2,
-               (int)n, pitch, g, ok);
-}
-
 void launch_row_nonzero(const double *v, long pitch, long n, int *flags, hipStream_t s) {
     MGX_LAUNCH(k_row_nonzero, dim3((unsigned)(n + 1)), dim3(256), s, v, pitch, n, flags);
 }

@@ -137,7 +137,6 @@ int materialize(mgx_ctx *c, int l) {
 // last smoothing pass; *fused_norm tells the caller whether the norm was done.
 int op_prolong_add(mgx_ctx *c, int l);
 int op_restrict(mgx_ctx *c, int l);
-static mgx::VGen level_vgen(const mgx_ctx *c, int l);
 int op_smooth(mgx_ctx *c, int l, int sweeps, bool prolong, bool restrict_, bool norm,
               bool *fused_norm) {
     Level &L = c->lv[l];
@@ -165,7 +164,6 @@ int op_smooth(mgx_ctx *c, int l, int sweeps, bool prolong, bool restrict_, bool 
             A.v2 = L.v2;
             A.zrow = c->zrow;
             A.vz = L.vz;
-            if (L.vgen && g_vgen) A.vg = level_vgen(c, l);
             A.n = L.n;
             A.pitch = L.pitch;
             A.c = L.coef;
@@ -189,7 +187,7 @@ int op_smooth(mgx_ctx *c, int l, int sweeps, bool prolong, bool restrict_, bool 
             // coarse u read (prolong) / coarse rhs written (restrict)
             // (v1 / v2 rows >= vz come from the zero row, not HBM)
             const double cbytes = 8.0 * (((mode & mgx::kModeZero) ? 2.0 : 3.0) * L.M() +
-                                         ((L.vgen && g_vgen) ? 0.0 : 2.0 * L.Mv()) +
+                                         2.0 * L.Mv() +
                                          ((pr ? 1 : 0) + (rs ? 1 : 0)) * c->lv[l + 1].M());
             int blocks = 0;
             CHK(launch(c, kind, l, bytes, cbytes,
@@ -701,57 +699,6 @@ int find_zero_rows(mgx_ctx *c) {
     return rc;
 }
 
-// tuning key "vgen": 1 = coarse levels whose velocity rows are the
-// reference tower's re-read of the finest rank-1 field (checked entry by
-// entry at upload) regenerate them from the finest level's factors in the
-// V-cycle's wave-march passes instead of reading them; 0 = read them
-long g_vgen = 0;
-
-static mgx::VGen level_vgen(const mgx_ctx *c, int l) {
-    mgx::VGen g;
-    const Level &F = c->lv[0];
-    g.a1 = F.sa1;
-    g.b1 = F.sb1;
-    g.a2 = F.sa2;
-    g.b2 = F.sb2;
-    g.N = (int)c->N;
-    g.W = (int)(c->N / 4 + 1);
-    g.l = l;
-    return g;
-}
-
-// Levels 1..3 whose rows [0, vz) equal the generator's values bitwise
-// (reference tower, finest factors present): Level::vgen.
-int find_vgen_levels(mgx_ctx *c) {
-    for (auto &L : c->lv) L.vgen = false;
-    const Level &F = c->lv[0];
-    if (c->opt.tower_mode != MGX_TOWER_REFERENCE || !F.sa1 || c->L < 2 || (c->N & 3) ||
-        c->N > 32768)
-        return MGX_OK;
-    int *dok = nullptr;
-    HIPCHK(hipMalloc(&dok, sizeof(int) * 4));
-    int rc = MGX_OK;
-    const int top = std::min(c->L - 1, 3);
-    std::vector<int> ones(top + 1, 1), h(top + 1, 0);
-    if (hipMemcpyAsync(dok, ones.data(), sizeof(int) * (top + 1), hipMemcpyHostToDevice,
-                       c->stream) != hipSuccess)
-        rc = fail(MGX_E_HIP, "find_vgen_levels");
-    for (int l = 1; l <= top && rc == MGX_OK; ++l) {
-        Level &L = c->lv[l];
-        mgx::launch_vgen_check(L.v1, L.v2, L.n, L.pitch, L.vz, level_vgen(c, l), dok + l,
-                               c->stream);
-        rc = check_launch("vgen_check");
-    }
-    if (rc == MGX_OK &&
-        (hipMemcpyAsync(h.data(), dok, sizeof(int) * (top + 1), hipMemcpyDeviceToHost,
-                        c->stream) != hipSuccess ||
-         hipStreamSynchronize(c->stream) != hipSuccess))
-        rc = fail(MGX_E_HIP, "find_vgen_levels");
-    (void)hipFree(dok);
-    for (int l = 1; l <= top && rc == MGX_OK; ++l) c->lv[l].vgen = h[l] == 1;
-    return rc;
-}
-
 void free_ctx(mgx_ctx *c) {
     if (!c) return;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
@@ -987,7 +934,6 @@ int mgxi::upload_ctx(mgx_ctx *c, const double *u0, const double *v1, const doubl
     if (kind == hipMemcpyHostToDevice && c->L > 1 && c->N >= kCrossMinN &&
         factor_velocity(v1, v2, c->N, 0, c->N + 1, L.coef.h * 0.5, a1, b1, a2, b2))
         CHK(set_level_factors(L, 0, a1, b1, a2, b2, c->stream));
-    CHK(find_vgen_levels(c));
     HIPCHK(hipStreamSynchronize(c->stream));
     return MGX_OK;
 }
@@ -1391,10 +1337,7 @@ extern "C" int mgx_factor_velocity(const double *v, long rows, long n, double sm
 // reads rhs and u only)
 extern "C" int mgx_velocity_factored(mgx_ctx *c, int *factored) {
     if (!c || !factored) return fail(MGX_E_ARG, "mgx_velocity_factored: bad args");
-    int f = (!c->lv.empty() && c->lv[0].sa1) ? 1 : 0;
-    for (size_t l = 1; l < c->lv.size() && l < 31; ++l)
-        if (c->lv[l].vgen && mgxi::g_vgen) f |= 1 << l;
-    *factored = f;
+    *factored = (!c->lv.empty() && c->lv[0].sa1) ? 1 : 0;
     return MGX_OK;
 }
 
@@ -1423,11 +1366,6 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
     if (!strcmp(key, "dist_min_rows")) {
         if (value < 16 || (value & 1)) return fail(MGX_E_ARG, "dist_min_rows must be even, >= 16");
         mgxi::g_dist_min_rows = value;
-        return MGX_OK;
-    }
-    if (!strcmp(key, "vgen")) {
-        if (value != 0 && value != 1) return fail(MGX_E_ARG, "vgen must be 0 or 1");
-        mgxi::g_vgen = value;
         return MGX_OK;
     }
     if (!strcmp(key, "xfast")) {
@@ -1528,10 +1466,6 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "dist_min_rows")) {
         *value = mgxi::g_dist_min_rows;
-        return MGX_OK;
-    }
-    if (!strcmp(key, "vgen")) {
-        *value = mgxi::g_vgen;
         return MGX_OK;
     }
     if (!strcmp(key, "xfast")) {

@@ -187,32 +187,6 @@ constexpr int kFinalThreads = 1024;
 //
 // Work split (marches): a 1-D grid of workgroups, each with a share of the
 // (strip, row) space (MarchRegions below), so one launch is one balanced wave.
-// Level-0 flat index of the reference tower's level-l entry (i, j) (VGen,
-// kernels.h), or -1 where the tower holds zero.  l <= 3 steps of the
-// injection, 32-bit (every index < (N+1)^2 < 2^31 for N <= 32768).
-__device__ __forceinline__ int vgen_index(const VGen &g, int i, int j, int nl) {
-    if (j > nl) return -1;
-    const unsigned W = (unsigned)g.W, W2 = W * W, sp = 2u * W - 1u;
-    unsigned m = (unsigned)i * (unsigned)(nl + 1) + (unsigned)j;
-    for (int s = 0; s < g.l; ++s) {
-        if (m >= W2) return -1;
-        const unsigned I = m / W, J = m - I * W;
-        m = 2u * I * sp + 2u * J;
-    }
-    return (int)m;
-}
-// v1 and v2 of the entry: fl(a[r] * b[c]), r, c = divmod(k, N+1)
-__device__ __forceinline__ void vgen_value(const VGen &g, int k, double &x, double &y) {
-    if (k < 0) {
-        x = y = 0.0;
-        return;
-    }
-    const unsigned np = (unsigned)g.N + 1u;
-    const unsigned r = (unsigned)k / np, cc = (unsigned)k - r * np;
-    x = g.a1[r] * g.b1[cc];
-    y = g.a2[r] * g.b2[cc];
-}
-
 struct RowData {
     double2 r, x, y;
 };

@@ -95,16 +95,13 @@ struct WCfg {
 // the stages contract (four fmas), residuals
 // are d*(update - u); RHSN's rhs keeps the reference expressions (gs.cpp:44,
 // stored unscaled) and is scaled after.
-// VG: rows < vz of v1 / v2 regenerated from the finest level's factors
-// (the reference tower, VGen in kernels.h): bitwise the stored rows, read
-// from two L2-resident 1-D arrays per field instead of two 2-D rows.
-template <int WPB, int K, int MODE, bool G, bool PD = false, bool FM = false, bool VG = false>
+template <int WPB, int K, int MODE, bool G, bool PD = false, bool FM = false>
 __global__ __launch_bounds__(64 * WPB, (WCfg<K, MODE>::MINB)) void k_wsmooth(
     const double *__restrict__ uin, double *__restrict__ uout, const double *__restrict__ rhs,
     const double *__restrict__ v1, const double *__restrict__ v2, const double *__restrict__ uc,
     long pitchc, double *__restrict__ rhsc, double *__restrict__ partials, int n, long pitch,
     MarchRegions reg, long units_per_wg, Coef c, int lo, int hi, double *__restrict__ rhs_out,
-    const double *__restrict__ zrow, int vz, VGen vg) {
+    const double *__restrict__ zrow, int vz) {
     using C = WCfg<K, MODE>;
     constexpr int S = C::S, E = C::E, H = C::H, NR = C::NR, W = C::W;
     // rhs/v prefetch distance in steps (row s+WRV takes the slot of row
@@ -208,16 +205,8 @@ __global__ __launch_bounds__(64 * WPB, (WCfg<K, MODE>::MINB)) void k_wsmooth(
             const long o = rowoff(Rc, ip);
             if (!C::RHSN) d.r = ld2((rhs + o) + cl);
             const bool z = Rc >= vz;
-            if (VG && !z) {
-                double x0, y0, x1, y1;
-                vgen_value(vg, vgen_index(vg, Rc, cl, n), x0, y0);
-                vgen_value(vg, vgen_index(vg, Rc, cl + 1, n), x1, y1);
-                d.x = make_double2(x0, x1);
-                d.y = make_double2(y0, y1);
-            } else {
-                d.x = ld2((z ? zrow : v1 + o) + cl);
-                d.y = ld2((z ? zrow : v2 + o) + cl);
-            }
+            d.x = ld2((z ? zrow : v1 + o) + cl);
+            d.y = ld2((z ? zrow : v2 + o) + cl);
         };
         // (FM: and f' = f/d; RHSN forms the rhs after this, see rhs_norm)
         auto scale_rv = [&](RowData &d) {
@@ -662,7 +651,7 @@ __global__ __launch_bounds__(MGX_TILE_THREADS) void k_smooth_tile(
 
 }  // namespace
 
-template <int WPB, int K, int MODE, bool G, bool PD, bool FM, bool VG = false>
+template <int WPB, int K, int MODE, bool G, bool PD, bool FM>
 static int wsmooth_launch_pd(const SmoothArgs &A, const MarchRegions &reg, double *partials,
                              long max_wgs, hipStream_t s) {
     const long total = reg.pre[reg.count];
@@ -672,8 +661,8 @@ static int wsmooth_launch_pd(const SmoothArgs &A, const MarchRegions &reg, doubl
         int dev = 0, cus = 0, per = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per, k_wsmooth<WPB, K, MODE, G, PD, FM, VG>, 64 * WPB, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_wsmooth<WPB, K, MODE, G, PD, FM>,
+                                                           64 * WPB, 0);
         slots = std::max(1, cus) * std::max(1, per);
     }
     long upw;
@@ -684,10 +673,9 @@ static int wsmooth_launch_pd(const SmoothArgs &A, const MarchRegions &reg, doubl
     // strips); the same per rank on 8 row blocks
     const unsigned grid = plan_march(reg, WPB, slots, get_march_min_rows(), max_wgs,
                                      WCfg<K, MODE>::E + WCfg<K, MODE>::NR / 2, upw, r);
-    MGX_LAUNCH((k_wsmooth<WPB, K, MODE, G, PD, FM, VG>), dim3(grid), dim3(64 * WPB), s, A.uin,
-               A.uout, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch, r,
-               upw, A.c, A.lo, A.hi, A.rhs_out, A.zrow ? A.zrow : A.v1,
-               A.zrow ? A.vz : 0x7fffffff, A.vg);
+    MGX_LAUNCH((k_wsmooth<WPB, K, MODE, G, PD, FM>), dim3(grid), dim3(64 * WPB), s, A.uin, A.uout,
+               A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch, r, upw,
+               A.c, A.lo, A.hi, A.rhs_out, A.zrow ? A.zrow : A.v1, A.zrow ? A.vz : 0x7fffffff);
     return (int)grid * WPB;   // NORM partials written
 }
 // the short division when the diagonal is positive (every nu <= 0)
@@ -695,15 +683,6 @@ template <int WPB, int K, int MODE, bool G>
 static int wsmooth_launch(const SmoothArgs &A, const MarchRegions &reg, double *partials,
                           long max_wgs, hipStream_t s) {
     // (fp_mode fma: no division)
-    // the reference tower's velocity generator on the V-cycle's coarse passes
-    constexpr bool VGM = (MODE == 2 || MODE == 5) && G;
-    if (VGM && A.vg.a1 && A.zrow) {
-        if (A.c.fm)
-            return wsmooth_launch_pd<WPB, K, MODE, G, false, true, VGM>(A, reg, partials, max_wgs, s);
-        if (A.c.dgs > 0)
-            return wsmooth_launch_pd<WPB, K, MODE, G, true, false, VGM>(A, reg, partials, max_wgs, s);
-        return wsmooth_launch_pd<WPB, K, MODE, G, false, false, VGM>(A, reg, partials, max_wgs, s);
-    }
     if (A.c.fm) return wsmooth_launch_pd<WPB, K, MODE, G, false, true>(A, reg, partials, max_wgs, s);
     if (A.c.dgs > 0)
         return wsmooth_launch_pd<WPB, K, MODE, G, true, false>(A, reg, partials, max_wgs, s);

@@ -201,11 +201,6 @@ int mgx_synchronize(mgx_ctx *ctx);
  * "xfast": 1 (default) runs the cross-cycle pass as an unguarded kernel over
  * the interior strips and rows plus a guarded kernel over the boundary strips
  * and bands; 0 = one guarded launch (bitwise the same results).
- * "vgen": 1 = coarse levels 1-3 whose nonzero velocity rows are the
- * reference tower's re-read of a rank-1 finest field (checked entry by entry
- * at upload) regenerate those rows from the finest level's factors in the
- * V-cycle's row-march passes instead of reading them from HBM; 0 (default)
- * = read them.  Bitwise the same results.
  * "march_tile_rows": a row block whose wave march would give each resident
  * workgroup fewer than this many rows runs as LDS tiles (default 16, >= 0).
  * "xtile_max_rows": on row blocks of at most this many rows (a rank of a
@@ -266,8 +261,7 @@ int mgx_set_tuning(const char *key, long value);
  * returns 1 and fills a[rows], b[n+1] with fl(a[i]*b[j]) == v[i][j] (same
  * bits) and every nonzero |v|, |b| still normal after scaling by smin, else 0. */
 int mgx_factor_velocity(const double *v, long rows, long n, double smin, double *a, double *b);
-/* *factored: bit 0 = the context keeps velocity factors for its finest level;
- * bit l (1..3) = level l regenerates its velocity rows from them ("vgen"). */
+/* *factored = 1 when the context keeps velocity factors for its finest level. */
 int mgx_velocity_factored(mgx_ctx *ctx, int *factored);
 int mgx_get_tuning(const char *key, long *value);
 
