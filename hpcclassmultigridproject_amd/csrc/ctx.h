@@ -48,6 +48,9 @@ struct Level {
     // rows >= vz of v1 and v2 are all zeros (found at upload): the row march
     // reads them from mgx_ctx::zrow (L2-resident) instead of HBM
     int vz = 0x7fffffff;
+    // level 1 of the reference tower: v1 / v2 equal the generator's entries
+    // from the finest factors (checked at upload, stencil.h vg_col)
+    bool vgen = false;
     mgx::Coef coef{};
     double M() const { return double(n + 1) * double(n + 1); }
     // compulsory bytes of v1 + v2 of this level (the zero rows cost no HBM)
@@ -80,6 +83,7 @@ struct mgx_ctx {
     double *hscal = nullptr;      // pinned host mirror
     double *stage[2] = {nullptr, nullptr};   // reference-layout (N+1)^2 staging
     double *zrow = nullptr;   // one row of zeros (finest pitch): Level::vz rows read it
+    double2 *vga = nullptr;   // VGen::a of level 1 (Level::vgen), N+2 pairs
     mgxi::Dist *dist = nullptr;   // row-partitioned multi-GPU state (dist.hip)
     // mg_outer's cycle predicted to be the last: its finest level runs the
     // post-smoothing alone, not the cross pass (no next-cycle pre-smoothing)

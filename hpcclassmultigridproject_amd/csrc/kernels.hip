@@ -141,6 +141,27 @@ __global__ __launch_bounds__(256) void k_row_nonzero(const double *v, long pitch
     if (threadIdx.x == 0) flags[blockIdx.x] = any;
 }
 
+// Level 1 entry (i = blockIdx.y, j) against the generator (stencil.h vg_col):
+// the same operands the wave march multiplies, compared bit for bit
+__global__ __launch_bounds__(256) void k_vgen_check(const double *v1, const double *v2, int n,
+                                                    long pitch, VGen g, int *ok) {
+    const int j = blockIdx.x * 256 + threadIdx.x, i = blockIdx.y;
+    if (j > n) return;
+    const VGCol k = vg_col(j, n);
+    const int st = vg_state(k, i), I = vg_row(k, i, st, 2 * n);
+    if (I < 0 || I > 2 * n + 1) {
+        *ok = 0;
+        return;
+    }
+    const int c = st == 1 ? k.clo : k.chi;
+    const double2 a = g.a[I];
+    const double x = a.x * (st == 2 ? 0.0 : g.b1[c]), y = a.y * (st == 2 ? 0.0 : g.b2[c]);
+    const long o = (long)i * pitch + j;
+    if (__double_as_longlong(x) != __double_as_longlong(v1[o]) ||
+        __double_as_longlong(y) != __double_as_longlong(v2[o]))
+        *ok = 0;   // benign: every writer stores 0
+}
+
 // Interior sum of squares, rows split over the grid; deterministic per block.
 __global__ __launch_bounds__(256) void k_norm_partial(const double *res, long n, long pitch,
                                                       int rows_per_block, double *partials) {
@@ -673,6 +694,12 @@ void launch_injection_rows(double *dst, long dst_pitch, const double *src, long 
 
 void launch_row_nonzero(const double *v, long pitch, long n, int *flags, hipStream_t s) {
     MGX_LAUNCH(k_row_nonzero, dim3((unsigned)(n + 1)), dim3(256), s, v, pitch, n, flags);
+}
+
+void launch_vgen_check(const double *v1, const double *v2, long n, long pitch, VGen g, int *ok,
+                       hipStream_t s) {
+    MGX_LAUNCH(k_vgen_check, dim3((unsigned)((n + 256) / 256), (unsigned)(n + 1)), dim3(256), s,
+               v1, v2, (int)n, pitch, g, ok);
 }
 
 int norm_partials_size() { return kNormBlocks; }

@@ -137,6 +137,18 @@ int materialize(mgx_ctx *c, int l) {
 // last smoothing pass; *fused_norm tells the caller whether the norm was done.
 int op_prolong_add(mgx_ctx *c, int l);
 int op_restrict(mgx_ctx *c, int l);
+// tuning key "vgen": 1 (default) = level 1 of the reference tower, when its
+// velocity passed the upload check (find_vgen), generates v1 / v2 in the
+// V-cycle's 3-sweep passes from the finest factors instead of reading them
+// (stencil.h vg_col; bitwise the same); 0 = reads them
+long g_vgen = 1;
+static mgx::VGen level1_vgen(const mgx_ctx *c) {
+    mgx::VGen g;
+    g.a = c->vga;
+    g.b1 = c->lv[0].sb1;
+    g.b2 = c->lv[0].sb2;
+    return g;
+}
 int op_smooth(mgx_ctx *c, int l, int sweeps, bool prolong, bool restrict_, bool norm,
               bool *fused_norm) {
     Level &L = c->lv[l];
@@ -164,6 +176,7 @@ int op_smooth(mgx_ctx *c, int l, int sweeps, bool prolong, bool restrict_, bool 
             A.v2 = L.v2;
             A.zrow = c->zrow;
             A.vz = L.vz;
+            if (L.vgen && g_vgen) A.vg = level1_vgen(c);
             A.n = L.n;
             A.pitch = L.pitch;
             A.c = L.coef;
@@ -186,8 +199,12 @@ int op_smooth(mgx_ctx *c, int l, int sweeps, bool prolong, bool restrict_, bool 
             // compulsory: u (unless zero), rhs, v1, v2 read, u written, the
             // coarse u read (prolong) / coarse rhs written (restrict)
             // (v1 / v2 rows >= vz come from the zero row, not HBM)
+            // (generated velocity: the 3-sweep pre / post marches, launch_smooth)
+            const bool vgu = A.vg.a && k == 3 && L.n > mgx::get_tile_max_n() &&
+                             (mode == (mgx::kModeZero | mgx::kModeRestrict) ||
+                              mode == mgx::kModeProlong);
             const double cbytes = 8.0 * (((mode & mgx::kModeZero) ? 2.0 : 3.0) * L.M() +
-                                         2.0 * L.Mv() +
+                                         (vgu ? 0.0 : 2.0 * L.Mv()) +
                                          ((pr ? 1 : 0) + (rs ? 1 : 0)) * c->lv[l + 1].M());
             int blocks = 0;
             CHK(launch(c, kind, l, bytes, cbytes,
@@ -699,6 +716,47 @@ int find_zero_rows(mgx_ctx *c) {
     return rc;
 }
 
+// Level 1 generates its velocity (Level::vgen) when the tower is the
+// reference's, the finest factors exist and every level-1 entry equals the
+// generator's bits (k_vgen_check).  a1, a2: the finest row factors.
+int find_vgen(mgx_ctx *c, const std::vector<double> &a1, const std::vector<double> &a2) {
+    for (auto &L : c->lv) L.vgen = false;
+    (void)hipFree(c->vga);
+    c->vga = nullptr;
+    const Level &F = c->lv[0];
+    if (c->opt.tower_mode != MGX_TOWER_REFERENCE || !F.sa1 || c->L < 2 || (c->N & 3) ||
+        c->N > 32768 || c->lv[1].n * 2 != c->N || (long)a1.size() != c->N + 1 ||
+        (long)a2.size() != c->N + 1)
+        return MGX_OK;
+    std::vector<double2> h((size_t)c->N + 2, make_double2(0.0, 0.0));
+    for (long I = 0; I <= c->N; ++I) h[(size_t)I] = make_double2(a1[(size_t)I], a2[(size_t)I]);
+    HIPCHK(hipMalloc(&c->vga, sizeof(double2) * h.size()));
+    int *dok = nullptr;
+    HIPCHK(hipMalloc(&dok, sizeof(int)));
+    int ok = 0, one = 1;
+    int rc = MGX_OK;
+    Level &L1 = c->lv[1];
+    if (hipMemcpyAsync(c->vga, h.data(), sizeof(double2) * h.size(), hipMemcpyHostToDevice,
+                       c->stream) != hipSuccess ||
+        hipMemcpyAsync(dok, &one, sizeof(int), hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        rc = fail(MGX_E_HIP, "find_vgen");
+    if (rc == MGX_OK) {
+        mgx::launch_vgen_check(L1.v1, L1.v2, L1.n, L1.pitch, level1_vgen(c), dok, c->stream);
+        rc = check_launch("vgen_check");
+    }
+    if (rc == MGX_OK &&
+        (hipMemcpyAsync(&ok, dok, sizeof(int), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+         hipStreamSynchronize(c->stream) != hipSuccess))
+        rc = fail(MGX_E_HIP, "find_vgen");
+    (void)hipFree(dok);
+    L1.vgen = rc == MGX_OK && ok == 1;
+    if (!L1.vgen) {
+        (void)hipFree(c->vga);
+        c->vga = nullptr;
+    }
+    return rc;
+}
+
 void free_ctx(mgx_ctx *c) {
     if (!c) return;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
@@ -718,6 +776,7 @@ void free_ctx(mgx_ctx *c) {
     (void)hipFree(c->stage[0]);
     (void)hipFree(c->stage[1]);
     (void)hipFree(c->zrow);
+    (void)hipFree(c->vga);
     if (c->hscal) (void)hipHostFree(c->hscal);
     for (auto &r : c->pending) {
         (void)hipEventDestroy(r.e0);
@@ -934,6 +993,7 @@ int mgxi::upload_ctx(mgx_ctx *c, const double *u0, const double *v1, const doubl
     if (kind == hipMemcpyHostToDevice && c->L > 1 && c->N >= kCrossMinN &&
         factor_velocity(v1, v2, c->N, 0, c->N + 1, L.coef.h * 0.5, a1, b1, a2, b2))
         CHK(set_level_factors(L, 0, a1, b1, a2, b2, c->stream));
+    CHK(find_vgen(c, a1, a2));
     HIPCHK(hipStreamSynchronize(c->stream));
     return MGX_OK;
 }
@@ -1337,7 +1397,9 @@ extern "C" int mgx_factor_velocity(const double *v, long rows, long n, double sm
 // reads rhs and u only)
 extern "C" int mgx_velocity_factored(mgx_ctx *c, int *factored) {
     if (!c || !factored) return fail(MGX_E_ARG, "mgx_velocity_factored: bad args");
-    *factored = (!c->lv.empty() && c->lv[0].sa1) ? 1 : 0;
+    int f = (!c->lv.empty() && c->lv[0].sa1) ? 1 : 0;
+    if (c->lv.size() > 1 && c->lv[1].vgen && mgxi::g_vgen) f |= 2;
+    *factored = f;
     return MGX_OK;
 }
 
@@ -1433,6 +1495,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgxi::g_sep_velocity = value;
         return MGX_OK;
     }
+    if (!strcmp(key, "vgen")) {
+        if (value != 0 && value != 1) return fail(MGX_E_ARG, "vgen must be 0 or 1");
+        mgxi::g_vgen = value;
+        return MGX_OK;
+    }
     if (!strcmp(key, "zero_rows")) {
         if (value != 0 && value != 1) return fail(MGX_E_ARG, "zero_rows must be 0 or 1");
         mgxi::g_zero_rows = value;
@@ -1518,6 +1585,10 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "sep_velocity")) {
         *value = mgxi::g_sep_velocity;
+        return MGX_OK;
+    }
+    if (!strcmp(key, "vgen")) {
+        *value = mgxi::g_vgen;
         return MGX_OK;
     }
     if (!strcmp(key, "zero_rows")) {

@@ -190,6 +190,45 @@ constexpr int kFinalThreads = 1024;
 struct RowData {
     double2 r, x, y;
 };
+
+// Level 1 of the reference tower (multigrid.cpp:148-160) as the
+// finest rank-1 velocity re-read: with n = N/2, W = N/4 + 1, the entry (i, j)
+// is the finest entry (I, c) = (2i + q, 2j - q(2W-1)), q = floor((j-i)/W),
+// where i(2W-1) + j < W^2, and zero beyond (the injection's zero fill).  So
+// v1(i, j) = fl(sa1[I] * sb1[c]) bit for bit wherever the finest field is its
+// exact factors (checked entry by entry at upload, launch_vgen_check).  For a
+// fixed column j, as the march goes down the rows, q takes at most two values
+// (the nonzero rows, i < ~W/2, span less than W): state 0 (q = qh =
+// floor(j/W)) for i < rt, state 1 (q = qh - 1) for rt <= i < rz, state 2
+// (zero) for i >= rz.  (VGen: kernels.h.)
+struct VGCol {
+    int qh, rt, rz, chi, clo;   // chi / clo: the finest column of states 0 / 1
+};
+__host__ __device__ inline VGCol vg_col(int j, int n) {
+    VGCol k;
+    const int W = n / 2 + 1, den = 2 * W - 1, N = 2 * n;
+    if (j < 0 || j > n) {   // outside the level: every row zero
+        k.qh = 0;
+        k.rt = 0;
+        k.rz = -0x7fffffff;
+        k.chi = k.clo = 0;
+        return k;
+    }
+    k.qh = j / W;
+    k.rt = j - k.qh * W + 1;
+    k.rz = (W * W - j + den - 1) / den;
+    const int chi = 2 * j - k.qh * den, clo = chi + den;
+    k.chi = chi < 0 ? 0 : (chi > N ? N : chi);   // (an unused state's column: any valid)
+    k.clo = clo < 0 ? 0 : (clo > N ? N : clo);
+    return k;
+}
+__host__ __device__ inline int vg_state(const VGCol &k, int i) {
+    return i >= k.rz ? 2 : (i >= k.rt ? 1 : 0);
+}
+// the finest row I of state st (N+1: the zero entry of VGen::a)
+__host__ __device__ inline int vg_row(const VGCol &k, int i, int st, int N) {
+    return st == 2 ? N + 1 : 2 * i + k.qh - st;
+}
 // the four coefficients of a row's two points (column c0 in .x, c0+1 in .y):
 // (rhs - cn*uN - cw*uW - cs*uS - ce*uE) / d, gs.cpp:126-130
 struct CoefRow {

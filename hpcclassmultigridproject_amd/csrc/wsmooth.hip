@@ -95,14 +95,20 @@ struct WCfg {
 // the stages contract (four fmas), residuals
 // are d*(update - u); RHSN's rhs keeps the reference expressions (gs.cpp:44,
 // stored unscaled) and is scaled after.
-template <int WPB, int K, int MODE, bool G, bool PD = false, bool FM = false>
+// VG: level 1 of the reference tower, v1 / v2 generated from the finest
+// factors (stencil.h vg_col): per row two cached loads of the (sa1, sa2) pairs
+// of the lane's two columns replace the two HBM row loads; the lane's sb pairs
+// (three states per column) sit in its LDS slice and are multiplied in at the
+// row's first use -- the same operands as the tower's entries, bitwise.
+template <int WPB, int K, int MODE, bool G, bool PD = false, bool FM = false, bool VG = false>
 __global__ __launch_bounds__(64 * WPB, (WCfg<K, MODE>::MINB)) void k_wsmooth(
     const double *__restrict__ uin, double *__restrict__ uout, const double *__restrict__ rhs,
     const double *__restrict__ v1, const double *__restrict__ v2, const double *__restrict__ uc,
     long pitchc, double *__restrict__ rhsc, double *__restrict__ partials, int n, long pitch,
     MarchRegions reg, long units_per_wg, Coef c, int lo, int hi, double *__restrict__ rhs_out,
-    const double *__restrict__ zrow, int vz) {
+    const double *__restrict__ zrow, int vz, VGen vg) {
     using C = WCfg<K, MODE>;
+    __shared__ double2 vgl[VG ? 64 * WPB * 6 : 1];
     constexpr int S = C::S, E = C::E, H = C::H, NR = C::NR, W = C::W;
     // rhs/v prefetch distance in steps (row s+WRV takes the slot of row
     // s+WRV-NR, last used by the residual stage on row s+1-S); RHSN uses a
@@ -141,6 +147,18 @@ __global__ __launch_bounds__(64 * WPB, (WCfg<K, MODE>::MINB)) void k_wsmooth(
         const bool keep = act && l >= H && l < 64 - H;
         const bool in0 = act && c0 >= 1 && c0 <= n - 1;
         const bool in1 = act && c0 + 1 <= n - 1;
+        VGCol g0{}, g1{};
+        const int lb = threadIdx.x * 6;
+        if constexpr (VG) {   // (lane-private slice: no barrier)
+            g0 = vg_col(c0, n);
+            g1 = vg_col(c0 + 1, n);
+            vgl[lb + 0] = make_double2(vg.b1[g0.chi], vg.b2[g0.chi]);
+            vgl[lb + 1] = make_double2(vg.b1[g0.clo], vg.b2[g0.clo]);
+            vgl[lb + 2] = make_double2(0.0, 0.0);
+            vgl[lb + 3] = make_double2(vg.b1[g1.chi], vg.b2[g1.chi]);
+            vgl[lb + 4] = make_double2(vg.b1[g1.clo], vg.b2[g1.clo]);
+            vgl[lb + 5] = make_double2(0.0, 0.0);
+        }
 
         struct UPre {
             double2 X;
@@ -204,12 +222,25 @@ __global__ __launch_bounds__(64 * WPB, (WCfg<K, MODE>::MINB)) void k_wsmooth(
             const int Rc = min(max(R, lo), hi);
             const long o = rowoff(Rc, ip);
             if (!C::RHSN) d.r = ld2((rhs + o) + cl);
+            if constexpr (VG) {   // (sa1, sa2) of column c0 in x, c0+1 in y
+                d.x = vg.a[vg_row(g0, Rc, vg_state(g0, Rc), 2 * n)];
+                d.y = vg.a[vg_row(g1, Rc, vg_state(g1, Rc), 2 * n)];
+                return;
+            }
             const bool z = Rc >= vz;
             d.x = ld2((z ? zrow : v1 + o) + cl);
             d.y = ld2((z ? zrow : v2 + o) + cl);
         };
         // (FM: and f' = f/d; RHSN forms the rhs after this, see rhs_norm)
-        auto scale_rv = [&](RowData &d) {
+        auto scale_rv = [&](RowData &d, const int R) {
+            if constexpr (VG) {   // v = fl(a * b) of row R's states
+                const int Rc = min(max(R, lo), hi);
+                const double2 b0 = vgl[lb + vg_state(g0, Rc)];
+                const double2 b1 = vgl[lb + 3 + vg_state(g1, Rc)];
+                const double2 a0 = d.x, a1 = d.y;
+                d.x = make_double2(a0.x * b0.x, a1.x * b1.x);
+                d.y = make_double2(a0.y * b0.y, a1.y * b1.y);
+            }
             d.x = make_double2(d.x.x * hh, d.x.y * hh);
             d.y = make_double2(d.y.x * hh, d.y.y * hh);
             if (FM && !C::RHSN) d.r = make_double2(d.r.x * c.rdgs, d.r.y * c.rdgs);
@@ -305,7 +336,7 @@ __global__ __launch_bounds__(64 * WPB, (WCfg<K, MODE>::MINB)) void k_wsmooth(
             }
         };
         if (C::RHSN) {
-            scale_rv(rd[1]);
+            scale_rv(rd[1], s + 1);
             rhs_norm(s + 1, 1, 0, 2);   // the first stage's row
         }
 
@@ -316,7 +347,7 @@ __global__ __launch_bounds__(64 * WPB, (WCfg<K, MODE>::MINB)) void k_wsmooth(
                 ur[(p + 3) % NR] = make_u(s + 3, up[(p + 3) % NR], (p + 3) & 1);
                 load_u(s + 3 + WU, up[(p + 3 + WU) % NR], (p + 3 + WU) & 1);
                 // t of the row first used in this step: s+2 (RHSN), else s+1
-                scale_rv(rd[(p + (C::RHSN ? 2 : 1)) % NR]);
+                scale_rv(rd[(p + (C::RHSN ? 2 : 1)) % NR], s + (C::RHSN ? 2 : 1));
                 if (WH) {   // cn, cs of row s+1 from t1 (gs.cpp:128-129's cc, dd)
                     const RowData &d1 = rd[(p + 1) % NR];
                     CoefRow &k1 = cf[(p + 1) % NR];
@@ -651,7 +682,7 @@ __global__ __launch_bounds__(MGX_TILE_THREADS) void k_smooth_tile(
 
 }  // namespace
 
-template <int WPB, int K, int MODE, bool G, bool PD, bool FM>
+template <int WPB, int K, int MODE, bool G, bool PD, bool FM, bool VG>
 static int wsmooth_launch_pd(const SmoothArgs &A, const MarchRegions &reg, double *partials,
                              long max_wgs, hipStream_t s) {
     const long total = reg.pre[reg.count];
@@ -661,7 +692,7 @@ static int wsmooth_launch_pd(const SmoothArgs &A, const MarchRegions &reg, doubl
         int dev = 0, cus = 0, per = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_wsmooth<WPB, K, MODE, G, PD, FM>,
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_wsmooth<WPB, K, MODE, G, PD, FM, VG>,
                                                            64 * WPB, 0);
         slots = std::max(1, cus) * std::max(1, per);
     }
@@ -673,20 +704,22 @@ static int wsmooth_launch_pd(const SmoothArgs &A, const MarchRegions &reg, doubl
     // strips); the same per rank on 8 row blocks
     const unsigned grid = plan_march(reg, WPB, slots, get_march_min_rows(), max_wgs,
                                      WCfg<K, MODE>::E + WCfg<K, MODE>::NR / 2, upw, r);
-    MGX_LAUNCH((k_wsmooth<WPB, K, MODE, G, PD, FM>), dim3(grid), dim3(64 * WPB), s, A.uin, A.uout,
-               A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch, r, upw,
-               A.c, A.lo, A.hi, A.rhs_out, A.zrow ? A.zrow : A.v1, A.zrow ? A.vz : 0x7fffffff);
+    MGX_LAUNCH((k_wsmooth<WPB, K, MODE, G, PD, FM, VG>), dim3(grid), dim3(64 * WPB), s, A.uin,
+               A.uout, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n, A.pitch, r,
+               upw, A.c, A.lo, A.hi, A.rhs_out, A.zrow ? A.zrow : A.v1,
+               A.zrow ? A.vz : 0x7fffffff, A.vg);
     return (int)grid * WPB;   // NORM partials written
 }
 // the short division when the diagonal is positive (every nu <= 0)
-template <int WPB, int K, int MODE, bool G>
+template <int WPB, int K, int MODE, bool G, bool VG = false>
 static int wsmooth_launch(const SmoothArgs &A, const MarchRegions &reg, double *partials,
                           long max_wgs, hipStream_t s) {
     // (fp_mode fma: no division)
-    if (A.c.fm) return wsmooth_launch_pd<WPB, K, MODE, G, false, true>(A, reg, partials, max_wgs, s);
+    if (A.c.fm)
+        return wsmooth_launch_pd<WPB, K, MODE, G, false, true, VG>(A, reg, partials, max_wgs, s);
     if (A.c.dgs > 0)
-        return wsmooth_launch_pd<WPB, K, MODE, G, true, false>(A, reg, partials, max_wgs, s);
-    return wsmooth_launch_pd<WPB, K, MODE, G, false, false>(A, reg, partials, max_wgs, s);
+        return wsmooth_launch_pd<WPB, K, MODE, G, true, false, VG>(A, reg, partials, max_wgs, s);
+    return wsmooth_launch_pd<WPB, K, MODE, G, false, false, VG>(A, reg, partials, max_wgs, s);
 }
 
 // One guarded launch over the whole level.  (The interior / edge split that
@@ -698,6 +731,10 @@ static int smooth_winst(const SmoothArgs &A, hipStream_t s) {
     using C = WCfg<K, MODE>;
     MarchRegions inner, edge;
     march_regions<WPB>(A.n, C::W, C::H, A.ra, A.rb, C::TOP, C::BOT, false, inner, edge);
+    // the generated velocity: the V-cycle's 3-sweep pre / post passes
+    if constexpr (K == 3 && (MODE == (kModeZero | kModeRestrict) || MODE == kModeProlong))
+        if (A.vg.a) return wsmooth_launch<WPB, K, MODE, true, true>(A, edge, A.partials,
+                                                                     kNormBlocks / WPB, s);
     return wsmooth_launch<WPB, K, MODE, true>(A, edge, A.partials, kNormBlocks / WPB, s);
 }
 

@@ -91,7 +91,7 @@ TUNING_KEYS = {   # key -> (a valid value, an invalid value or None)
     "tile32_min_n": (1024, -1), "tile_xcd": (0, 2), "march_order": (1, 4),
     "march_min_rows": (96, 4), "coarse_lds": (0, 2), "step_fuse": (0, 2), "march_seg": (0, 2), "xtile_max_rows": (0, -1),
     "post_predict": (-1, -2), "post_only": (-1, -2), "step_cross": (0, 2),
-    "sep_velocity": (0, 2), "zero_rows": (0, 2), "march_tile_rows": (32, -1),
+    "sep_velocity": (0, 2), "zero_rows": (0, 2), "vgen": (0, 2), "march_tile_rows": (32, -1),
 }
 
 
