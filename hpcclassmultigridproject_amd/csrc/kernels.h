@@ -75,13 +75,14 @@ enum : int { kModeZero = 1, kModeProlong = 2, kModeRestrict = 4, kModeNorm = 8 }
 // and the residual norm of uin against it goes to *norm_out -- a time step's
 // compute_rhs, mg_outer's initial norm and the first pre-smoothing in one pass.
 constexpr int kModeRhsNorm = 16;
-// Velocity generator of level 1 of the reference tower (stencil.h vg_col):
-// its v1 / v2 entries from the finest level's exact factors
+// Velocity generator of level l (1 or 2) of the reference tower (stencil.h
+// vg_col): its v1 / v2 entries from the finest level's exact factors
 struct VGen {
     const double2 *a = nullptr;   // (sa1[I], sa2[I]), I = 0..N; (+0, +0) at N+1
     const double *b1 = nullptr, *b2 = nullptr;   // finest sb1, sb2 (0..N used)
+    int l = 1;
 };
-// clear *ok (device int) unless every entry (i, j <= n) of the level-1 fields
+// clear *ok (device int) unless every entry (i, j <= n) of level g.l's fields
 // v1, v2 (pitch) equals the generator's bits
 void launch_vgen_check(const double *v1, const double *v2, long n, long pitch, VGen g, int *ok,
                        hipStream_t s);
@@ -102,7 +103,7 @@ struct SmoothArgs {
     // from zrow (one zero row of >= pitch doubles, L2-resident) instead of HBM
     const double *zrow = nullptr;
     int vz = 0x7fffffff;
-    // vg.a set (level 1 of the reference tower, checked at upload): the
+    // vg.a set (level 1 or 2 of the reference tower, checked at upload): the
     // 3-sweep pre / post passes generate v1, v2 instead of reading them
     VGen vg{};
     bool norm_sqrt = true;

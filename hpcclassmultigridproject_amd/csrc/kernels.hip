@@ -141,15 +141,15 @@ __global__ __launch_bounds__(256) void k_row_nonzero(const double *v, long pitch
     if (threadIdx.x == 0) flags[blockIdx.x] = any;
 }
 
-// Level 1 entry (i = blockIdx.y, j) against the generator (stencil.h vg_col):
-// the same operands the wave march multiplies, compared bit for bit
+// Level g.l entry (i = blockIdx.y, j) against the generator (stencil.h
+// vg_col): the same operands the wave march multiplies, compared bit for bit
 __global__ __launch_bounds__(256) void k_vgen_check(const double *v1, const double *v2, int n,
                                                     long pitch, VGen g, int *ok) {
-    const int j = blockIdx.x * 256 + threadIdx.x, i = blockIdx.y;
+    const int j = blockIdx.x * 256 + threadIdx.x, i = blockIdx.y, N = n << g.l;
     if (j > n) return;
-    const VGCol k = vg_col(j, n);
-    const int st = vg_state(k, i), I = vg_row(k, i, st, 2 * n);
-    if (I < 0 || I > 2 * n + 1) {
+    const VGCol k = vg_col(j, n, g.l);
+    const int st = vg_state(k, i), I = vg_row(k, i, st, g.l, N);
+    if (I < 0 || I > N + 1) {
         *ok = 0;
         return;
     }

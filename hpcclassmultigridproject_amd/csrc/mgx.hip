@@ -137,16 +137,17 @@ int materialize(mgx_ctx *c, int l) {
 // last smoothing pass; *fused_norm tells the caller whether the norm was done.
 int op_prolong_add(mgx_ctx *c, int l);
 int op_restrict(mgx_ctx *c, int l);
-// tuning key "vgen": 1 (default) = level 1 of the reference tower, when its
-// velocity passed the upload check (find_vgen), generates v1 / v2 in the
+// tuning key "vgen": 1 (default) = levels 1-2 of the reference tower, when
+// their velocity passed the upload check (find_vgen), generate v1 / v2 in the
 // V-cycle's 3-sweep passes from the finest factors instead of reading them
 // (stencil.h vg_col; bitwise the same); 0 = reads them
 long g_vgen = 1;
-static mgx::VGen level1_vgen(const mgx_ctx *c) {
+static mgx::VGen level_vgen(const mgx_ctx *c, int l) {
     mgx::VGen g;
     g.a = c->vga;
     g.b1 = c->lv[0].sb1;
     g.b2 = c->lv[0].sb2;
+    g.l = l;
     return g;
 }
 int op_smooth(mgx_ctx *c, int l, int sweeps, bool prolong, bool restrict_, bool norm,
@@ -176,7 +177,7 @@ int op_smooth(mgx_ctx *c, int l, int sweeps, bool prolong, bool restrict_, bool 
             A.v2 = L.v2;
             A.zrow = c->zrow;
             A.vz = L.vz;
-            if (L.vgen && g_vgen) A.vg = level1_vgen(c);
+            if (L.vgen && g_vgen) A.vg = level_vgen(c, l);
             A.n = L.n;
             A.pitch = L.pitch;
             A.c = L.coef;
@@ -716,41 +717,50 @@ int find_zero_rows(mgx_ctx *c) {
     return rc;
 }
 
-// Level 1 generates its velocity (Level::vgen) when the tower is the
-// reference's, the finest factors exist and every level-1 entry equals the
-// generator's bits (k_vgen_check).  a1, a2: the finest row factors.
+// Levels 1-2 generate their velocity (Level::vgen) when the tower is the
+// reference's, the finest factors exist and every entry of the level equals
+// the generator's bits (k_vgen_check).  a1, a2: the finest row factors.
 int find_vgen(mgx_ctx *c, const std::vector<double> &a1, const std::vector<double> &a2) {
     for (auto &L : c->lv) L.vgen = false;
     (void)hipFree(c->vga);
     c->vga = nullptr;
     const Level &F = c->lv[0];
     if (c->opt.tower_mode != MGX_TOWER_REFERENCE || !F.sa1 || c->L < 2 || (c->N & 3) ||
-        c->N > 32768 || c->lv[1].n * 2 != c->N || (long)a1.size() != c->N + 1 ||
-        (long)a2.size() != c->N + 1)
+        c->N > 32768 || (long)a1.size() != c->N + 1 || (long)a2.size() != c->N + 1)
         return MGX_OK;
     std::vector<double2> h((size_t)c->N + 2, make_double2(0.0, 0.0));
     for (long I = 0; I <= c->N; ++I) h[(size_t)I] = make_double2(a1[(size_t)I], a2[(size_t)I]);
     HIPCHK(hipMalloc(&c->vga, sizeof(double2) * h.size()));
     int *dok = nullptr;
-    HIPCHK(hipMalloc(&dok, sizeof(int)));
-    int ok = 0, one = 1;
+    HIPCHK(hipMalloc(&dok, sizeof(int) * 3));
+    const int top = std::min(c->L - 1, 2);
+    int ok[3] = {0, 0, 0}, one[3] = {1, 1, 1};
     int rc = MGX_OK;
-    Level &L1 = c->lv[1];
     if (hipMemcpyAsync(c->vga, h.data(), sizeof(double2) * h.size(), hipMemcpyHostToDevice,
                        c->stream) != hipSuccess ||
-        hipMemcpyAsync(dok, &one, sizeof(int), hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        hipMemcpyAsync(dok, one, sizeof(one), hipMemcpyHostToDevice, c->stream) != hipSuccess)
         rc = fail(MGX_E_HIP, "find_vgen");
-    if (rc == MGX_OK) {
-        mgx::launch_vgen_check(L1.v1, L1.v2, L1.n, L1.pitch, level1_vgen(c), dok, c->stream);
+    for (int l = 1; l <= top && rc == MGX_OK; ++l) {
+        const Level &L = c->lv[l];
+        if ((L.n << l) != c->N || (L.n & 1)) {
+            ok[l] = 0;
+            continue;
+        }
+        mgx::launch_vgen_check(L.v1, L.v2, L.n, L.pitch, level_vgen(c, l), dok + l, c->stream);
         rc = check_launch("vgen_check");
     }
     if (rc == MGX_OK &&
-        (hipMemcpyAsync(&ok, dok, sizeof(int), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        (hipMemcpyAsync(ok, dok, sizeof(ok), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
          hipStreamSynchronize(c->stream) != hipSuccess))
         rc = fail(MGX_E_HIP, "find_vgen");
     (void)hipFree(dok);
-    L1.vgen = rc == MGX_OK && ok == 1;
-    if (!L1.vgen) {
+    bool any = false;
+    for (int l = 1; l <= top && rc == MGX_OK; ++l) {
+        Level &L = c->lv[l];
+        L.vgen = (L.n << l) == c->N && !(L.n & 1) && ok[l] == 1;
+        any = any || L.vgen;
+    }
+    if (!any) {
         (void)hipFree(c->vga);
         c->vga = nullptr;
     }
@@ -1398,7 +1408,8 @@ extern "C" int mgx_factor_velocity(const double *v, long rows, long n, double sm
 extern "C" int mgx_velocity_factored(mgx_ctx *c, int *factored) {
     if (!c || !factored) return fail(MGX_E_ARG, "mgx_velocity_factored: bad args");
     int f = (!c->lv.empty() && c->lv[0].sa1) ? 1 : 0;
-    if (c->lv.size() > 1 && c->lv[1].vgen && mgxi::g_vgen) f |= 2;
+    for (size_t l = 1; l < c->lv.size() && l < 3; ++l)
+        if (c->lv[l].vgen && mgxi::g_vgen) f |= 1 << l;
     *factored = f;
     return MGX_OK;
 }

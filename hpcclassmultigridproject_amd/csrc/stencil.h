@@ -191,22 +191,24 @@ struct RowData {
     double2 r, x, y;
 };
 
-// Level 1 of the reference tower (multigrid.cpp:148-160) as the
-// finest rank-1 velocity re-read: with n = N/2, W = N/4 + 1, the entry (i, j)
-// is the finest entry (I, c) = (2i + q, 2j - q(2W-1)), q = floor((j-i)/W),
-// where i(2W-1) + j < W^2, and zero beyond (the injection's zero fill).  So
-// v1(i, j) = fl(sa1[I] * sb1[c]) bit for bit wherever the finest field is its
-// exact factors (checked entry by entry at upload, launch_vgen_check).  For a
-// fixed column j, as the march goes down the rows, q takes at most two values
-// (the nonzero rows, i < ~W/2, span less than W): state 0 (q = qh =
-// floor(j/W)) for i < rt, state 1 (q = qh - 1) for rt <= i < rz, state 2
-// (zero) for i >= rz.  (VGen: kernels.h.)
+// Levels 1 and 2 of the reference tower (multigrid.cpp:148-160)
+// are re-reads of the finest rank-1 velocity through the injection's index
+// quirk: with s = 2^(l-1), W = N/4 + 1, level l's entry (i, j) is the finest
+// entry (I, c) = (2s i + q, 2s j - q(2W-1)) with q = floor(s(j-i)/W), where s(i(2W-1) + j) < W^2, and zero beyond (the
+// injection's zero fill).  So v1(i, j) = fl(sa1[I] * sb1[c]) bit for bit
+// wherever the finest field is its exact factors (checked entry by entry at
+// upload, launch_vgen_check).  For a fixed column j, as the march goes down
+// the rows, q takes at most two values (the nonzero rows, i < ~W/(2s), move
+// s(j-i) by less than W): state 0 (q = qh = floor(s j/W)) for i < rt, state
+// 1 (q = qh - 1) for rt <= i < rz, state 2 (zero) for i >= rz.  (VGen:
+// kernels.h; tests/test_vgen_formula.py checks the closed form against the
+// CPU checker's tower.)
 struct VGCol {
     int qh, rt, rz, chi, clo;   // chi / clo: the finest column of states 0 / 1
 };
-__host__ __device__ inline VGCol vg_col(int j, int n) {
+__host__ __device__ inline VGCol vg_col(int j, int n, int l) {
     VGCol k;
-    const int W = n / 2 + 1, den = 2 * W - 1, N = 2 * n;
+    const int N = n << l, W = N / 4 + 1, den = 2 * W - 1, s = 1 << (l - 1);
     if (j < 0 || j > n) {   // outside the level: every row zero
         k.qh = 0;
         k.rt = 0;
@@ -214,10 +216,10 @@ __host__ __device__ inline VGCol vg_col(int j, int n) {
         k.chi = k.clo = 0;
         return k;
     }
-    k.qh = j / W;
-    k.rt = j - k.qh * W + 1;
-    k.rz = (W * W - j + den - 1) / den;
-    const int chi = 2 * j - k.qh * den, clo = chi + den;
+    k.qh = s * j / W;
+    k.rt = (s * j - k.qh * W) / s + 1;
+    k.rz = (W * W - s * j + s * den - 1) / (s * den);
+    const int chi = 2 * s * j - k.qh * den, clo = chi + den;
     k.chi = chi < 0 ? 0 : (chi > N ? N : chi);   // (an unused state's column: any valid)
     k.clo = clo < 0 ? 0 : (clo > N ? N : clo);
     return k;
@@ -226,9 +228,10 @@ __host__ __device__ inline int vg_state(const VGCol &k, int i) {
     return i >= k.rz ? 2 : (i >= k.rt ? 1 : 0);
 }
 // the finest row I of state st (N+1: the zero entry of VGen::a)
-__host__ __device__ inline int vg_row(const VGCol &k, int i, int st, int N) {
-    return st == 2 ? N + 1 : 2 * i + k.qh - st;
+__host__ __device__ inline int vg_row(const VGCol &k, int i, int st, int l, int N) {
+    return st == 2 ? N + 1 : (i << l) + k.qh - st;
 }
+
 // the four coefficients of a row's two points (column c0 in .x, c0+1 in .y):
 // (rhs - cn*uN - cw*uW - cs*uS - ce*uE) / d, gs.cpp:126-130
 struct CoefRow {

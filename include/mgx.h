@@ -257,17 +257,18 @@ int mgx_set_tuning(const char *key, long value);
  * reference tower) are found, and the row marches read them from
  * one L2-resident zero row instead of HBM; 0 = every row from HBM (bitwise
  * the same results).
- * "vgen": 1 (default) = level 1 of the reference tower, whose v1 / v2 are a
- * re-read of the finest rank-1 field, generates them in the
+ * "vgen": 1 (default) = levels 1-2 of the reference tower, whose v1 / v2 are
+ * re-reads of the finest rank-1 field, generate them in the
  * V-cycle's 3-sweep smoothing passes from the finest level's factors instead
- * of reading them from HBM -- only when every level-1 entry equals the
- * generator's bits (checked at upload); 0 = reads them.  Bitwise the same. */
+ * of reading them from HBM -- only when every entry of the level equals the
+ * generator's bits (checked at upload, per level); 0 = reads them.  Bitwise
+ * the same. */
 /* Host only: exact rank-1 factors of v (rows x (n+1), row-major):
  * returns 1 and fills a[rows], b[n+1] with fl(a[i]*b[j]) == v[i][j] (same
  * bits) and every nonzero |v|, |b| still normal after scaling by smin, else 0. */
 int mgx_factor_velocity(const double *v, long rows, long n, double smin, double *a, double *b);
 /* *factored: bit 0 = the context keeps velocity factors for its finest level;
- * bit 1 = level 1 generates its velocity from them ("vgen"). */
+ * bits 1, 2 = level 1, 2 generates its velocity from them ("vgen"). */
 int mgx_velocity_factored(mgx_ctx *ctx, int *factored);
 int mgx_get_tuning(const char *key, long *value);
 

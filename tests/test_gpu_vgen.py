@@ -1,7 +1,7 @@
-"""Level 1's generated velocity (tuning key "vgen", kernels.h VGen, stencil.h
-vg_col): the V-cycle's 3-sweep pre / post marches of level 1 regenerate v1,
+"""Levels 1-2's generated velocity (tuning key "vgen", kernels.h VGen, stencil.h
+vg_col): the V-cycle's 3-sweep pre / post marches of levels 1-2 regenerate v1,
 v2 from the finest level's factors instead of reading them.  Enabled only
-when the upload check finds every level-1 entry equal to the generator's bits,
+when the upload check finds every entry of the level equal to the generator's bits,
 so u, norms and cycle counts must be BITWISE those of the read path, in both
 fp modes, for V-cycles (with the cross-cycle pass), plain cycles and time
 steps."""
@@ -44,10 +44,10 @@ def _run(N, L, fp, vgen, cycles=3, steps=2, tower=_lib.TOWER_REFERENCE, perturb=
 
 @pytest.mark.parametrize("fp", [_lib.FP_BITWISE, _lib.FP_FMA], ids=["bitwise", "fma"])
 @pytest.mark.parametrize("N,L", [(4096, 7), (16384, 9)])
-def test_generated_level1_velocity_bitwise_vs_read(N, L, fp):
+def test_generated_coarse_velocity_bitwise_vs_read(N, L, fp):
     fa, na, ua, ca, ub = _run(N, L, fp, 1)
     fb, nb, va, cb, vb = _run(N, L, fp, 0)
-    assert fa == 3, fa          # finest factors + level 1 generating
+    assert fa == 7, fa          # finest factors + levels 1, 2 generating
     assert fb == 1, fb
     assert na == nb
     assert np.array_equal(ua.view(np.uint64), va.view(np.uint64))
@@ -58,5 +58,5 @@ def test_generated_level1_velocity_bitwise_vs_read(N, L, fp):
 def test_no_generator_without_the_reference_tower_or_factors():
     # the correct tower (every level injected from the level above) is not the
     # re-read the generator reproduces; a non-rank-1 field has no factors
-    assert _run(4096, 7, _lib.FP_FMA, 1, cycles=1, steps=0, tower=_lib.TOWER_CORRECT)[0] & 2 == 0
+    assert _run(4096, 7, _lib.FP_FMA, 1, cycles=1, steps=0, tower=_lib.TOWER_CORRECT)[0] & 6 == 0
     assert _run(4096, 7, _lib.FP_FMA, 1, cycles=1, steps=0, perturb=True)[0] == 0
