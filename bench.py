@@ -536,9 +536,10 @@ def main():
         ofp = _lib.FP_BITWISE if fp == _lib.FP_FMA else _lib.FP_FMA
         other = side_run("bitwise" if ofp == _lib.FP_BITWISE else "fma", ofp, {}, 3)
         # the generic velocity path (2-D v1 / v2 on every row of every level:
-        # sep_velocity = zero_rows = 0): the headline reads the reference
-        # flow's exact rank-1 factors on level 0 and skips the coarse levels'
-        # all-zero velocity rows
+        # sep_velocity = zero_rows = 0, hence no generator either): the
+        # headline reads the reference flow's exact rank-1 factors on level 0,
+        # regenerates levels 1-2's velocity from them (vgen) and skips the
+        # coarser levels' all-zero velocity rows
         generic = side_run("generic velocity", fp, {"sep_velocity": 0, "zero_rows": 0}, 3)
         generic["note"] = "sep_velocity=0, zero_rows=0: every velocity row read from HBM"
 
@@ -604,8 +605,10 @@ def main():
                    "last_residual": res},
         "roofline": roof,
         "kernels": kernels,
-        "velocity": ("level 0: exact rank-1 factors (sep_velocity); coarse levels: all-zero "
-                     "rows from one L2-resident row (zero_rows)" if fac.value else
+        "velocity": ("level 0: exact rank-1 factors (sep_velocity); "
+                     + ("levels 1-2: regenerated from them (vgen); levels >= 3: "
+                        if fac.value & 6 else "coarse levels: ")
+                     + "all-zero rows from one L2-resident row (zero_rows)" if fac.value else
                      "2-D arrays"),
         "other_fp_mode": other,
         "generic_velocity_path": generic,
