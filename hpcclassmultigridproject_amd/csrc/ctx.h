@@ -157,6 +157,7 @@ int set_level_factors(Level &L, long row0, const std::vector<double> &a1,
                       const std::vector<double> &b2, hipStream_t s);
 void free_level_factors(Level &L);
 extern long g_sep_velocity;
+extern long g_vgen;   // tuning key "vgen" (mgx.hip)
 void free_ctx(mgx_ctx *c);
 // Create a single-GPU context; stream != nullptr: borrow that stream.
 int create_ctx(mgx_ctx **out, long n, int maxlvl, double dt, double nu, const mgx_options *opt,

@@ -98,6 +98,7 @@ struct PLevel {
     // (full-length arrays, this block's rows filled), or null
     double *sa1 = nullptr, *sb1 = nullptr, *sa2 = nullptr, *sb2 = nullptr;
     int vz = 0x7fffffff;   // Level::vz (global rows)
+    bool vgen = false;     // Level::vgen (levels 1-2: generated velocity)
     mgx::Coef coef{};
     int nxt() const { return cur == 0 ? 1 : 0; }
     // field pointer offset so that F(a) + r*pitch is global row r
@@ -114,6 +115,7 @@ struct Part {
     double *dsum = nullptr;   // device scalar: this rank's partial sum of squares
     double *partials = nullptr;   // this part's norm partials (a split pass keeps them
                                   // between its two launches while other parts run)
+    double2 *vga = nullptr;       // mgx_ctx::vga (levels with PLevel::vgen), or null
     hipEvent_t xe0 = nullptr;     // profiling: the start of a split pass
 };
 
@@ -165,6 +167,7 @@ void dist_free(mgx_ctx *c) {
             for (double *f : {L.sa1, L.sb1, L.sa2, L.sb2}) (void)hipFree(f);
         }
         if (p.sub) free_ctx(p.sub);
+        (void)hipFree(p.vga);
         (void)hipFree(p.dsum);
         (void)hipFree(p.partials);
     }
@@ -608,12 +611,22 @@ static int smooth(mgx_ctx *c, int l, bool prolong, bool restrict_, bool norm) {
             A.norm_sqrt = false;
             A.zrow = c->zrow;
             A.vz = L.vz;
+            // levels 1-2: velocity generated from level 0's factors (global
+            // rows and columns, the whole level's: dist_upload)
+            if (L.vgen && g_vgen && p.vga && p.lv[0].sb1) {
+                A.vg.a = p.vga;
+                A.vg.b1 = p.lv[0].sb1;
+                A.vg.b2 = p.lv[0].sb2;
+                A.vg.l = l;
+            }
+            const bool vgu = mgx::smooth_generates_velocity(A, k, mode);
             double bytes = 40.0 * k * L.Mown();
             const double Mc = L.Mown() / 4;
             if (pr) bytes += 32.0 * L.Mown() + 8.0 * Mc;
             if (rs) bytes += 40.0 * L.Mown() + 24.0 * Mc;
             if (nm) bytes += 48.0 * L.Mown();
-            const double cbytes = 8.0 * ((zero ? 4.0 : 5.0) * L.Mown() +
+            const double cbytes = 8.0 * ((zero ? 4.0 : 5.0) * L.Mown() -
+                                         (vgu ? 2.0 * L.Mown() : 0.0) +
                                          ((pr ? 1 : 0) + (rs ? 1 : 0)) * Mc);
             int blocks = 0;
             CHK(launch(c, pr ? MGX_K_PSMOOTH : MGX_K_GS, l, bytes, cbytes,
@@ -993,6 +1006,16 @@ int dist_upload(mgx_ctx *c, const double *u0, const double *v1, const double *v2
     CHK(create_ctx(&T, c->N, c->L, c->dt, c->nu, &o, c->stream));
     int rc = upload_ctx(T, u0, v1, v2, kind);
     for (auto &p : d->parts) {
+        // the generated velocity of levels 1-2 (checked over the whole level in T)
+        (void)hipFree(p.vga);
+        p.vga = nullptr;
+        if (rc == MGX_OK && T->vga) {
+            const size_t vb = sizeof(double2) * (size_t)(c->N + 2);
+            if (hipMalloc(&p.vga, vb) != hipSuccess ||
+                hipMemcpyAsync(p.vga, T->vga, vb, hipMemcpyDeviceToDevice, c->stream) !=
+                    hipSuccess)
+                rc = fail(MGX_E_HIP, "dist_upload: vgen table");
+        }
         for (int l = 0; rc == MGX_OK && l < d->la; ++l) {
             PLevel &L = p.lv[l];
             Level &F = T->lv[l];
@@ -1010,6 +1033,7 @@ int dist_upload(mgx_ctx *c, const double *u0, const double *v1, const double *v2
             L.spec = -1;
             L.zero = false;
             L.vz = F.vz;
+            L.vgen = F.vgen && p.vga;
             if (rc == MGX_OK && l == 0) {   // the whole level's velocity factors, if any
                 if (F.sa1)
                     rc = part_factors(L, F.sa1, F.sb1, F.sa2, F.sb2, 0, L.n + 1,
@@ -1163,6 +1187,7 @@ static int dist_upload_rows_impl(mgx_ctx *c, const double *const *u0s,
             L.spec = -1;
             L.zero = false;
             L.vz = 0x7fffffff;
+            L.vgen = false;   // (the correct tower is not the re-read it generates)
         }
         PLevel &L = p.lv[0];
         const size_t row = w * sizeof(double), rows = L.hi - L.lo + 1;

@@ -115,6 +115,9 @@ struct SmoothArgs {
     int ra = 0, rb = -1, lo = 0, hi = -1;
 };
 int launch_smooth(const SmoothArgs &a, int sweeps, int mode, hipStream_t s);
+// whether launch_smooth(a, sweeps, mode) generates v1, v2 (a.vg, the 3-sweep
+// pre / post wave marches) instead of reading them: the launch's byte count
+bool smooth_generates_velocity(const SmoothArgs &a, int sweeps, int mode);
 
 // Cross-cycle fused finest-level pass (k_xsmooth): post-smoothing of cycle k
 // (u_in + P(uc), `sweeps` sweeps, residual norm -> *norm_out as sqrt) into

@@ -201,9 +201,7 @@ int op_smooth(mgx_ctx *c, int l, int sweeps, bool prolong, bool restrict_, bool 
             // coarse u read (prolong) / coarse rhs written (restrict)
             // (v1 / v2 rows >= vz come from the zero row, not HBM)
             // (generated velocity: the 3-sweep pre / post marches, launch_smooth)
-            const bool vgu = A.vg.a && k == 3 && L.n > mgx::get_tile_max_n() &&
-                             (mode == (mgx::kModeZero | mgx::kModeRestrict) ||
-                              mode == mgx::kModeProlong);
+            const bool vgu = mgx::smooth_generates_velocity(A, k, mode);
             const double cbytes = 8.0 * (((mode & mgx::kModeZero) ? 2.0 : 3.0) * L.M() +
                                          (vgu ? 0.0 : 2.0 * L.Mv()) +
                                          ((pr ? 1 : 0) + (rs ? 1 : 0)) * c->lv[l + 1].M());

@@ -787,8 +787,9 @@ long g_march_tile_rows = 16;
 void set_march_tile_rows(long v) { g_march_tile_rows = v; }
 long get_march_tile_rows() { return g_march_tile_rows; }
 
+// whether the pass runs as LDS tiles (else the wave-private row march)
 template <int K, int MODE>
-static int smooth_block(const SmoothArgs &A, hipStream_t s) {
+static bool smooth_as_tiles(const SmoothArgs &A) {
     // the row march needs >= ~32 rows per wave to amortise its priming rows;
     // a row block too small to give every resident wave that much (a
     // partitioned level on many GPUs) runs as LDS tiles instead
@@ -807,6 +808,12 @@ static int smooth_block(const SmoothArgs &A, hipStream_t s) {
         const long groups = (A.n + 1 + W4 - 1) / W4;
         tile = groups * (A.rb - A.ra) < (long)slots * g_march_tile_rows;
     }
+    return tile;
+}
+
+template <int K, int MODE>
+static int smooth_block(const SmoothArgs &A, hipStream_t s) {
+    const bool tile = smooth_as_tiles<K, MODE>(A);
     if (tile) {
         const int g = smooth_tile_inst<K, MODE>(A, s);
         if (g > 0) return g;
@@ -830,6 +837,18 @@ static int smooth_k(const SmoothArgs &A, int mode, hipStream_t s) {
         case 20: return smooth_block<K, 20>(A, s);
         default: return -1;
     }
+}
+
+bool smooth_generates_velocity(const SmoothArgs &A0, int sweeps, int mode) {
+    if (!A0.vg.a || sweeps != 3) return false;
+    SmoothArgs A = A0;   // (the whole level: as launch_smooth)
+    if (A.rb < 0) {
+        A.ra = 0;
+        A.rb = (int)A.n + 1;
+    }
+    if (mode == (kModeZero | kModeRestrict)) return !smooth_as_tiles<3, kModeZero | kModeRestrict>(A);
+    if (mode == kModeProlong) return !smooth_as_tiles<3, kModeProlong>(A);
+    return false;
 }
 
 int launch_smooth(const SmoothArgs &A0, int sweeps, int mode, hipStream_t s) {

@@ -60,3 +60,39 @@ def test_no_generator_without_the_reference_tower_or_factors():
     # re-read the generator reproduces; a non-rank-1 field has no factors
     assert _run(4096, 7, _lib.FP_FMA, 1, cycles=1, steps=0, tower=_lib.TOWER_CORRECT)[0] & 6 == 0
     assert _run(4096, 7, _lib.FP_FMA, 1, cycles=1, steps=0, perturb=True)[0] == 0
+
+
+def _dist_run(vgen, parts, N=16384, L=9):
+    old = _lib.get_tuning("vgen")
+    _lib.set_tuning("vgen", vgen)
+    try:
+        u0, v1, v2 = init_problem(N)
+        with Multigrid(N, L, 1.0 / N / 10, NU, fp_mode=_lib.FP_FMA, local_parts=parts) as mg:
+            mg.upload(u0, v1, v2)
+            mg.rhs()
+            mg.profile(True)
+            norms = [mg.run_cycles(1) for _ in range(3)]
+            # compulsory bytes of levels 1-2's smoothing passes (launch accounting)
+            cb = [sum(mg.profile_get_ex(k, l)[3] for k in (_lib.K_GS, _lib.K_PSMOOTH))
+                  for l in (1, 2)]
+            mg.profile(False)
+            return norms, mg.download(np.empty_like(u0)), cb
+    finally:
+        _lib.set_tuning("vgen", old)
+
+
+@pytest.mark.parametrize("parts", [2, 8])
+def test_generated_velocity_on_row_blocks_bitwise(parts):
+    """Virtual ranks (the row-block code path, dist.hip): levels 1-2's blocks
+    generate their rows of the velocity from level 0's global factors --
+    bitwise the read path, and the passes' compulsory bytes drop by the two
+    velocity arrays."""
+    na, ua, ca = _dist_run(1, parts)
+    nb, ub, cb = _dist_run(0, parts)
+    assert na == nb
+    assert np.array_equal(ua.view(np.uint64), ub.view(np.uint64))
+    # (level 1 always marches; level 2's blocks at 8 parts may run as LDS
+    # tiles, which read the arrays)
+    assert ca[0] < 0.75 * cb[0] and ca[1] <= cb[1], (ca, cb)
+    if parts == 2:
+        assert ca[1] < 0.75 * cb[1], (ca, cb)
