@@ -75,19 +75,27 @@ def kernels_sha():
     return h.hexdigest()
 
 
+def loaded_kernels_sha():
+    """The kernel-sources sha256 the LOADED libmgx.so was built from
+    (mgx_build_id, stamped by csrc/Makefile): what a PMC profile must match."""
+    from hpcclassmultigridproject_amd import _lib
+    return _lib.build_id()["kernel_sources_sha256"]
+
+
 def traffic_profile(mode):
     """(path, kernels) of the newest profiles/*_hbm_traffic.json collected from
-    the kernel sources built now in fp mode `mode`, or (None, reason)."""
+    the kernel sources the loaded library was built from, in fp mode `mode`, or
+    (None, reason)."""
     import glob
-    sha = kernels_sha()
+    sha = loaded_kernels_sha()
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*hbm_traffic*.json")),
                    key=os.path.getmtime, reverse=True)
     for f in files:
         d = json.load(open(f))
         if d.get("kernel_sources_sha256") == sha and d.get("mode") == mode:
             return os.path.relpath(f, ROOT), d["kernels"]
-    return None, (f"no profiles/*_hbm_traffic.json ({mode}) matches the kernel sources' sha256 "
-                  f"{sha[:12]} (regenerate with tools/profile_round.sh)")
+    return None, (f"no profiles/*_hbm_traffic.json ({mode}) matches the loaded library's "
+                  f"kernel sources sha256 {sha[:12]} (regenerate with tools/profile_round.sh)")
 
 
 def lookup_traffic(knames, mode, field="hbm_bytes"):
@@ -152,7 +160,43 @@ def parse():
                          "serial and all usable cores; writes cudatime.txt, serialtime.txt, "
                          "omptime.txt ('N<TAB>seconds', what speedupplot.py reads)")
     ap.add_argument("--sweep-out", default="", help="--sweep: output file prefix")
+    ap.add_argument("--watchdog-s", type=float, default=300.0,
+                    help="N > 1: deadline of each phase that waits on peers (RCCL self-check, "
+                         "set-up, overlap pricing, timed region); on expiry the rank prints an "
+                         "error JSON line and exits 1 instead of hanging")
     return ap.parse_args()
+
+
+class Watchdog:
+    """A deadline on a phase that waits on the other ranks (N > 1): an RCCL hang
+    would otherwise stall the run silently until an outer time limit.  On
+    expiry: one error JSON line on stdout, then os._exit(1) (no exec, no GPU
+    call from the timer thread)."""
+
+    def __init__(self, phase, seconds, rank, world):
+        self.phase, self.seconds, self.rank, self.world = phase, seconds, rank, world
+        self.timer = None
+
+    def _fire(self):
+        print(json.dumps({"metric": "V-cycle grid-point-updates/sec at N=16384; achieved HBM "
+                                    "GB/s vs peak", "value": None, "n_gpus": self.world,
+                          "error": f"watchdog: phase '{self.phase}' exceeded "
+                                   f"{self.seconds:.0f} s on rank {self.rank}"}), flush=True)
+        sys.stderr.flush()
+        os._exit(1)
+
+    def __enter__(self):
+        if self.world > 1 and self.seconds > 0:
+            import threading
+            self.timer = threading.Timer(self.seconds, self._fire)
+            self.timer.daemon = True
+            self.timer.start()
+        return self
+
+    def __exit__(self, *exc):
+        if self.timer is not None:
+            self.timer.cancel()
+        return False
 
 
 def host_cpus():
@@ -288,8 +332,12 @@ def main():
         if world == 1 and args.gpus > 1:
             sys.exit("for --gpus > 1 launch with torch.distributed.run --nproc-per-node N")
     torch.cuda.set_device(local)
+    def watch(phase):
+        return Watchdog(phase, args.watchdog_s, rank, world)
+
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        with watch("init_process_group"):
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     def barrier():
         if world > 1:
@@ -300,7 +348,8 @@ def main():
         # libmgx's own RCCL transport with real peers vs a one-GPU context,
         # bitwise (small problem, before and outside the timed region)
         from hpcclassmultigridproject_amd import dist as mgdist
-        rccl_check = mgdist.rccl_selfcheck(world, rank, local)
+        with watch("rccl_selfcheck"):
+            rccl_check = mgdist.rccl_selfcheck(world, rank, local)
 
     N, L = args.N, args.levels
     if args.weak and world > 1:
@@ -312,6 +361,7 @@ def main():
     dt = 1.0 / N / 10
     fp = _lib.FP_FMA if args.fp_mode == "fma" else _lib.FP_BITWISE
     dist_kw = {}
+    setup_wd = watch("set-up (context, upload, warm-up)").__enter__()
     if world > 1:
         from hpcclassmultigridproject_amd import dist as mgdist
         dist_kw = dict(world=world, rank=rank, unique_id=mgdist.broadcast_unique_id())
@@ -340,6 +390,7 @@ def main():
     for _ in range(args.warmup):
         mg.run_cycles(1)
     mg.synchronize()
+    setup_wd.__exit__(None, None, None)
 
     def max_over_ranks(x):
         if world == 1:
@@ -360,6 +411,7 @@ def main():
                         if rccl_check["modes"].get(str(m), {}).get("bitwise", False)] or [0]
         if args.overlap == "auto":
             overlap_ab = {}
+            wd = watch("overlap pricing").__enter__()
             for ov in ok_modes:
                 _lib.set_tuning("dist_overlap", ov)
                 mg.run_cycles(1)
@@ -369,6 +421,7 @@ def main():
                 mg.run_cycles(3)
                 mg.synchronize()
                 overlap_ab[ov] = round(max_over_ranks(time.perf_counter() - t0) / 3 * 1e3, 4)
+            wd.__exit__(None, None, None)
             best_ov = min(overlap_ab, key=overlap_ab.get)
         else:
             best_ov = int(args.overlap)
@@ -410,7 +463,8 @@ def main():
                 best = (kind, 0, n, ms, b, cb)
         return best
 
-    rep_s, res = timed_reps(mg, args.reps, not args.no_profile)
+    with watch("timed region"):
+        rep_s, res = timed_reps(mg, args.reps, not args.no_profile)
     elapsed = sorted(rep_s)[len(rep_s) // 2]   # the median repetition
     best = dominant(mg)
     mg.profile(False)
@@ -559,14 +613,15 @@ def main():
     if roof is not None and fac.value and world == 1:
         # the same pass's bytes if v1, v2 were read as 2-D arrays (the
         # reference algorithm's inputs, SURVEY 8(d): GS reads u, rhs, v1, v2):
-        # the velocity factors regenerate them bitwise instead of reading them
+        # the velocity factors regenerate them bitwise instead of reading them.
+        # An equivalent rate only -- no kernel moved these bytes, so no fraction
         vb = 2.0 * 8.0 * (N + 1) * ((N + 1 + 15) // 16 * 16)
         a2 = (roof["compulsory_bytes_per_launch"] + vb) / (roof["avg_launch_ms"] * 1e-3) / 1e9
         roof["algorithmic_2d_velocity"] = {
             "bytes_per_launch": roof["compulsory_bytes_per_launch"] + vb,
-            "GBs": round(a2, 1), "frac": round(a2 / HBM_PEAK_GBS, 4),
+            "equiv_GBs": round(a2, 1),
             "note": "compulsory bytes with v1, v2 counted as read (they are regenerated "
-                    "bitwise from their rank-1 factors instead)"}
+                    "bitwise from their rank-1 factors instead, not moved)"}
     reps_ms = [x / args.steps * 1e3 for x in rep_s]
     out = {
         "metric": f"V-cycle grid-point-updates/sec at N={N}; achieved HBM GB/s vs peak",
@@ -613,6 +668,13 @@ def main():
         "other_fp_mode": other,
         "generic_velocity_path": generic,
     }
+    # what the loaded library was built from (csrc/Makefile stamps it): the
+    # traffic lookup above used its kernel sha, not the tree's
+    bid = _lib.build_id()
+    bid["matches_tree"] = bid["kernel_sources_sha256"] == kernels_sha()
+    out["build"] = bid
+    if other is not None:   # the reference's bits, the library default, beside the headline
+        out["value_bitwise" if fp == _lib.FP_FMA else "value_fma"] = other["value"]
     if rccl_check is not None:
         out["rccl_parity"] = rccl_check
     if rank == 0 and world == 1 and args.cpu_baseline != "off":

@@ -100,6 +100,8 @@ _SIGS = {
     "mgx_write_uT": (_I, [C.c_char_p, _vp, _L, _L, _L, _I, _I]),
     "mgx_factor_velocity": (_I, [_vp, _L, _L, _D, _vp, _vp]),
     "mgx_velocity_factored": (_I, [_vp, C.POINTER(_I)]),
+    "mgx_build_id": (C.c_char_p, []),
+    "mgx_build_sources_id": (C.c_char_p, []),
 }
 
 _lib = None
@@ -145,6 +147,16 @@ def get_tuning(key: str) -> int:
     v = C.c_long()
     check(lib().mgx_get_tuning(key.encode(), C.byref(v)))
     return v.value
+
+
+def build_id() -> dict:
+    """What the loaded library was built from (mgx_build_id): the sha256 of its
+    kernel sources and of all its sources, and its path (MGX_LIB if set)."""
+    L = lib()
+    return {"kernel_sources_sha256": L.mgx_build_id().decode(),
+            "sources_sha256": L.mgx_build_sources_id().decode(),
+            "lib": os.path.relpath(LIB_PATH, os.path.dirname(HERE)),
+            "MGX_LIB": os.environ.get("MGX_LIB")}
 
 
 def stream_bandwidth(bytes_per_stream=1 << 30, nin=1, reps=10) -> float:

@@ -48,8 +48,9 @@ struct Level {
     // rows >= vz of v1 and v2 are all zeros (found at upload): the row march
     // reads them from mgx_ctx::zrow (L2-resident) instead of HBM
     int vz = 0x7fffffff;
-    // level 1 of the reference tower: v1 / v2 equal the generator's entries
-    // from the finest factors (checked at upload, stencil.h vg_col)
+    // levels 1-2 of the reference tower, levels >= 1 of the correct one: v1 /
+    // v2 equal the generator's entries from the finest factors (checked at
+    // upload, stencil.h vg_col)
     bool vgen = false;
     mgx::Coef coef{};
     double M() const { return double(n + 1) * double(n + 1); }
@@ -83,7 +84,7 @@ struct mgx_ctx {
     double *hscal = nullptr;      // pinned host mirror
     double *stage[2] = {nullptr, nullptr};   // reference-layout (N+1)^2 staging
     double *zrow = nullptr;   // one row of zeros (finest pitch): Level::vz rows read it
-    double2 *vga = nullptr;   // VGen::a of level 1 (Level::vgen), N+2 pairs
+    double2 *vga = nullptr;   // VGen::a of the Level::vgen levels, N+2 pairs
     mgxi::Dist *dist = nullptr;   // row-partitioned multi-GPU state (dist.hip)
     // mg_outer's cycle predicted to be the last: its finest level runs the
     // post-smoothing alone, not the cross pass (no next-cycle pre-smoothing)
@@ -151,7 +152,7 @@ int find_zero_rows(mgx_ctx *c);
 // of width n+1); false: not separable (or "sep_velocity" off), nothing set
 bool factor_velocity(const double *v1, const double *v2, long n, long r0, long rows, double smin,
                      std::vector<double> &a1, std::vector<double> &b1, std::vector<double> &a2,
-                     std::vector<double> &b2);
+                     std::vector<double> &b2, long *js1 = nullptr, long *js2 = nullptr);
 int set_level_factors(Level &L, long row0, const std::vector<double> &a1,
                       const std::vector<double> &b1, const std::vector<double> &a2,
                       const std::vector<double> &b2, hipStream_t s);
@@ -183,6 +184,7 @@ void dist_free(mgx_ctx *c);
 int dist_nsub(mgx_ctx *c);
 mgx_ctx *dist_sub(mgx_ctx *c, int i);
 int dist_la(mgx_ctx *c);
+int dist_velocity_mask(mgx_ctx *c);   // mgx_velocity_factored of a partitioned context
 // levels whose row blocks would be shorter than this are replicated (tuning
 // key "dist_min_rows", default 256)
 extern long g_dist_min_rows;
@@ -192,6 +194,7 @@ extern long g_dist_overlap;
 // tuning key "dist_local_side" (dist.hip): virtual ranks' early exchanges on
 // the compute stream (0) or the second stream (1)
 extern long g_dist_local_side;
+extern long g_dist_comm_chain;   // tuning key "dist_comm_chain" (test hook)
 // tuning key "cross_cycle" (mgx.hip); levels with n >= kCrossMinN can use it
 bool cross_cycle_on();
 constexpr long kCrossMinN = 4096;

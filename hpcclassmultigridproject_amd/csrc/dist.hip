@@ -16,7 +16,9 @@
 // Two transports with the same partition logic:
 //   * RCCL (mgx_create_dist): one process per GPU, ncclSend/ncclRecv of whole
 //     ghost-row blocks (contiguous in the pitched layout) to rank +-1 over
-//     xGMI, ncclAllGather / ncclAllReduce, all on the context stream;
+//     xGMI, ncclAllGather / ncclAllReduce -- ONE communicator, and at most one
+//     of its operations in flight per rank: each is chained after the
+//     previous one (comm_op), whichever of the two streams issues it;
 //   * local (mgx_create_local_dist): `world` virtual ranks in one process on
 //     one device, exchanges as device-to-device copies -- for testing the
 //     partitioned solver against the single-GPU one on a one-GPU machine.
@@ -59,6 +61,12 @@ long g_dist_overlap = -1;
 // cost a bubble, +5 % per cycle at G = 8) or on the second stream as over
 // RCCL (1: exercises the fork / join logic on one GPU).  Bitwise the same.
 long g_dist_local_side = 0;
+// tuning key "dist_comm_chain": 1 (default) = every RCCL operation of a rank is
+// ordered after its previous one (comm_op); 0 = a TEST HOOK that drops the
+// chain, so tests/test_gpu_fake_rccl.py can show that the fake RCCL's
+// happens-before check catches two operations in flight at once.  Never 0 on
+// real peers: NCCL operations of one communicator must not run concurrently.
+long g_dist_comm_chain = 1;
 
 // the partition / exchange plan (plan.h, host-only)
 using mgxplan::alloc_rows;
@@ -98,7 +106,10 @@ struct PLevel {
     // (full-length arrays, this block's rows filled), or null
     double *sa1 = nullptr, *sb1 = nullptr, *sa2 = nullptr, *sb2 = nullptr;
     int vz = 0x7fffffff;   // Level::vz (global rows)
-    bool vgen = false;     // Level::vgen (levels 1-2: generated velocity)
+    bool vgen = false;     // Level::vgen (generated velocity)
+    // level 0 of a row-block upload: the columns whose entries are the row
+    // factors of v1 / v2 (sepvel.h j*), or -1
+    long js1 = -1, js2 = -1;
     mgx::Coef coef{};
     int nxt() const { return cur == 0 ? 1 : 0; }
     // field pointer offset so that F(a) + r*pitch is global row r
@@ -124,11 +135,16 @@ struct Dist {
     bool local = false;
     int la = 0;
     std::vector<Part> parts;   // local: `world` parts; RCCL: this rank's part
+    // ONE communicator for every operation, compute stream and side stream
+    // alike.  NCCL runs the operations of a communicator in the order they are
+    // issued and they must not overlap; two communicators in flight at once
+    // "might work provided they fit within the GPU" and can deadlock otherwise
+    // (round-4 verdict).  So every operation goes through comm_op, which chains
+    // it after the rank's previous one: ev_comm is recorded after each, and an
+    // operation issued on the other stream than its predecessor waits for it.
     ncclComm_t comm = nullptr;
-    // the side stream's exchanges (dist_overlap) run on their own communicator,
-    // split from `comm` (same ranks): NCCL operations of one communicator must
-    // not run concurrently from two streams, those of two communicators may
-    ncclComm_t comm_x = nullptr;
+    hipEvent_t ev_comm = nullptr;      // end of this rank's last RCCL operation
+    hipStream_t comm_last = nullptr;   // the stream that issued it
     double *hsum = nullptr;    // pinned
     double *dsum_all = nullptr;   // virtual ranks: the parts' sums added (device)
     // dist_overlap: ghost exchanges on a second stream beside the interior pass
@@ -143,11 +159,15 @@ struct Dist {
     std::vector<int> early_buf;
     std::vector<hipEvent_t> ev_lvl;
     std::vector<char> lvl_pending;
+    // dist_overlap, per partitioned level l: its restricted rhs ghosts are
+    // being exchanged on the side stream (the level-1 rhs after the cross pass,
+    // behind the norm's host round trip); ev_rhs[l] marks the end
+    std::vector<hipEvent_t> ev_rhs;
+    std::vector<char> rhs_pending;
 };
 
 // the effective dist_overlap of a context (-1: by transport)
 static long overlap_mode(const Dist *d) {
-    if (d->comm && !d->comm_x) return 0;   // no side-stream communicator
     if (g_dist_overlap >= 0) return g_dist_overlap;
     return d->comm ? 1 : 0;
 }
@@ -171,12 +191,14 @@ void dist_free(mgx_ctx *c) {
         (void)hipFree(p.dsum);
         (void)hipFree(p.partials);
     }
-    if (d->comm_x) (void)ncclCommDestroy(d->comm_x);
     if (d->comm) (void)ncclCommDestroy(d->comm);
+    if (d->ev_comm) (void)hipEventDestroy(d->ev_comm);
     if (d->xs) (void)hipStreamDestroy(d->xs);
     if (d->ev_fork) (void)hipEventDestroy(d->ev_fork);
     if (d->ev_join) (void)hipEventDestroy(d->ev_join);
     for (hipEvent_t e : d->ev_lvl)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : d->ev_rhs)
         if (e) (void)hipEventDestroy(e);
     if (d->hsum) (void)hipHostFree(d->hsum);
     (void)hipFree(d->dsum_all);
@@ -203,6 +225,10 @@ static int build_dist(mgx_ctx *c, int world, const std::vector<int> &ranks) {
     d->lvl_pending.assign(d->la, 0);
     d->ev_lvl.assign(d->la, nullptr);
     for (auto &e : d->ev_lvl) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    d->rhs_pending.assign(d->la, 0);
+    d->ev_rhs.assign(d->la, nullptr);
+    for (auto &e : d->ev_rhs) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&d->ev_comm, hipEventDisableTiming));
     for (int r : ranks) {
         Part p;
         p.rank = r;
@@ -322,6 +348,21 @@ struct XF {
     int buf = -1;   // kU: this u buffer instead of the current one
 };
 
+// Issue one RCCL operation (a group, a collective) of this rank on stream st,
+// chained after the rank's previous one: if that was issued on another stream,
+// st first waits for its end (ev_comm).  Host issue order is the program order,
+// the same on every rank, so the ranks' operations pair up in order and no two
+// of one rank ever run at once -- whichever stream each was issued on.
+template <class F>
+static int comm_op(Dist *d, hipStream_t st, F &&issue) {
+    if (g_dist_comm_chain && d->comm_last && d->comm_last != st)
+        HIPCHK(hipStreamWaitEvent(st, d->ev_comm, 0));
+    CHK(issue());
+    HIPCHK(hipEventRecord(d->ev_comm, st));
+    d->comm_last = st;
+    return MGX_OK;
+}
+
 static int exchange_rows(mgx_ctx *c, const std::vector<XF> &xs, hipStream_t st) {
     Dist *d = c->dist;
     std::vector<Xfer> plan;
@@ -345,28 +386,29 @@ static int exchange_rows(mgx_ctx *c, const std::vector<XF> &xs, hipStream_t st) 
         return cb.flush(st);
     }
     Part &p = d->parts[0];
-    ncclComm_t comm = st == d->xs ? d->comm_x : d->comm;
-    if (!comm) return fail(MGX_E_INTERNAL, "ghost exchange: no communicator for this stream");
-    ncclResult_t r = ncclGroupStart();
-    for (const XF &x : xs) {
-        PLevel &L = p.lv[x.l];
-        const long P = L.pitch;
-        double *a = field(L, x.f, x.buf);
-        ghost_plan(c->N, x.l, d->world, p.rank, plan);
-        for (const Xfer &t : plan) {
-            if (r != ncclSuccess) break;
-            r = ncclSend(a + (long)t.send_row * P, (size_t)t.send_rows * P, ncclDouble, t.peer,
-                         comm, st);
-            if (r == ncclSuccess)
-                r = ncclRecv(a + (long)t.recv_row * P, (size_t)t.recv_rows * P, ncclDouble,
-                             t.peer, comm, st);
+    if (!d->comm) return fail(MGX_E_INTERNAL, "ghost exchange: no communicator");
+    return comm_op(d, st, [&]() -> int {
+        ncclResult_t r = ncclGroupStart();
+        for (const XF &x : xs) {
+            PLevel &L = p.lv[x.l];
+            const long P = L.pitch;
+            double *a = field(L, x.f, x.buf);
+            ghost_plan(c->N, x.l, d->world, p.rank, plan);
+            for (const Xfer &t : plan) {
+                if (r != ncclSuccess) break;
+                r = ncclSend(a + (long)t.send_row * P, (size_t)t.send_rows * P, ncclDouble,
+                             t.peer, d->comm, st);
+                if (r == ncclSuccess)
+                    r = ncclRecv(a + (long)t.recv_row * P, (size_t)t.recv_rows * P, ncclDouble,
+                                 t.peer, d->comm, st);
+            }
         }
-    }
-    const ncclResult_t re = ncclGroupEnd();   // always close the group
-    if (r == ncclSuccess) r = re;
-    if (r != ncclSuccess)
-        return fail(MGX_E_RCCL, std::string("ghost exchange: ") + ncclGetErrorString(r));
-    return MGX_OK;
+        const ncclResult_t re = ncclGroupEnd();   // always close the group
+        if (r == ncclSuccess) r = re;
+        if (r != ncclSuccess)
+            return fail(MGX_E_RCCL, std::string("ghost exchange: ") + ncclGetErrorString(r));
+        return MGX_OK;
+    });
 }
 
 // bytes moved by the parts this process holds: every row sent is read once
@@ -399,6 +441,7 @@ static int settle(mgx_ctx *c) {
     HIPCHK(hipStreamWaitEvent(c->stream, d->ev_join, 0));
     d->early_pending = false;
     std::fill(d->lvl_pending.begin(), d->lvl_pending.end(), 0);
+    std::fill(d->rhs_pending.begin(), d->rhs_pending.end(), 0);
     return MGX_OK;
 }
 
@@ -465,6 +508,17 @@ static int take_fresh(mgx_ctx *c, int l, bool *fresh) {
     return MGX_OK;
 }
 
+// The compute stream waits for a side-stream exchange of level l's rhs ghosts
+// (rhs_side), if one is pending.
+static int take_rhs(mgx_ctx *c, int l) {
+    Dist *d = c->dist;
+    if (l < d->la && d->rhs_pending[l]) {
+        HIPCHK(hipStreamWaitEvent(c->stream, d->ev_rhs[l], 0));
+        d->rhs_pending[l] = 0;
+    }
+    return MGX_OK;
+}
+
 // Restricted rhs of the first replicated level: every rank wrote its own rows
 // of the full array in its sub-context; make them whole everywhere.
 static int gather_rhs(mgx_ctx *c) {
@@ -488,18 +542,24 @@ static int gather_rhs(mgx_ctx *c) {
             const long P = p.sub->lv[0].pitch;
             double *rhs = p.sub->lv[0].rhs;
             // in place: the send buffer is the receive buffer + rank * count
-            NCCLCHK(ncclAllGather(rhs + row0 * P, rhs, (size_t)q * P, ncclDouble, d->comm,
-                                  c->stream));
+            CHK(comm_op(d, c->stream, [&]() -> int {
+                NCCLCHK(ncclAllGather(rhs + row0 * P, rhs, (size_t)q * P, ncclDouble, d->comm,
+                                      c->stream));
+                return MGX_OK;
+            }));
         }
     }
     for (auto &p : d->parts) p.sub->lv[0].zero = true;   // u[la] = 0 (multigrid.cpp:77)
     return MGX_OK;
 }
 
-// Sum the ranks' partial sums of squares -> norm on the host.
-static int reduce_norm(mgx_ctx *c, double *norm) {
+// Sum the ranks' partial sums of squares -> norm on the host, in two halves:
+// norm_issue enqueues the sum (all-reduce) and its read-back on the compute
+// stream, norm_finish waits for it.  The cross pass issues its norm BEFORE the
+// exchanges that follow it, so those run behind the host round trip instead of
+// in front of the all-reduce (comm_op orders them after it).
+static int norm_issue(mgx_ctx *c) {
     Dist *d = c->dist;
-    double tot = 0.0;
     if (d->local) {
         PtrList pl{};
         for (size_t i = 0; i < d->parts.size(); ++i) {
@@ -513,17 +573,26 @@ static int reduce_norm(mgx_ctx *c, double *norm) {
         }
         HIPCHK(hipMemcpyAsync(d->hsum, d->dsum_all, sizeof(double), hipMemcpyDeviceToHost,
                               c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
-        tot = d->hsum[0];
     } else {
         Part &p = d->parts[0];
-        NCCLCHK(ncclAllReduce(p.dsum, p.dsum, 1, ncclDouble, ncclSum, d->comm, c->stream));
+        CHK(comm_op(d, c->stream, [&]() -> int {
+            NCCLCHK(ncclAllReduce(p.dsum, p.dsum, 1, ncclDouble, ncclSum, d->comm, c->stream));
+            return MGX_OK;
+        }));
         HIPCHK(hipMemcpyAsync(d->hsum, p.dsum, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
-        tot = d->hsum[0];
     }
-    *norm = std::sqrt(tot);
     return MGX_OK;
+}
+
+static int norm_finish(mgx_ctx *c, double *norm) {
+    HIPCHK(hipStreamSynchronize(c->stream));
+    *norm = std::sqrt(c->dist->hsum[0]);
+    return MGX_OK;
+}
+
+static int reduce_norm(mgx_ctx *c, double *norm) {
+    CHK(norm_issue(c));
+    return norm_finish(c, norm);
 }
 
 // ---------------------------------------------------------------- V-cycle
@@ -567,6 +636,7 @@ static int smooth(mgx_ctx *c, int l, bool prolong, bool restrict_, bool norm) {
     const bool ca = post_ca(c);
     bool fresh = false;   // u ghosts exchanged early (dist_overlap)
     CHK(take_fresh(c, l, &fresh));
+    CHK(take_rhs(c, l));
     for (int done = 0; done < sweeps;) {
         const int k = std::min(sweeps - done, fuse);
         const bool first = done == 0, last = done + k == sweeps;
@@ -611,22 +681,25 @@ static int smooth(mgx_ctx *c, int l, bool prolong, bool restrict_, bool norm) {
             A.norm_sqrt = false;
             A.zrow = c->zrow;
             A.vz = L.vz;
-            // levels 1-2: velocity generated from level 0's factors (global
-            // rows and columns, the whole level's: dist_upload)
+            // velocity generated from level 0's factors (global rows and
+            // columns; dist_upload / the row-block upload's vgen_rows)
             if (L.vgen && g_vgen && p.vga && p.lv[0].sb1) {
                 A.vg.a = p.vga;
                 A.vg.b1 = p.lv[0].sb1;
                 A.vg.b2 = p.lv[0].sb2;
                 A.vg.l = l;
+                A.vg.strided = c->opt.tower_mode == MGX_TOWER_CORRECT ? 1 : 0;
             }
             const bool vgu = mgx::smooth_generates_velocity(A, k, mode);
-            double bytes = 40.0 * k * L.Mown();
-            const double Mc = L.Mown() / 4;
-            if (pr) bytes += 32.0 * L.Mown() + 8.0 * Mc;
-            if (rs) bytes += 40.0 * L.Mown() + 24.0 * Mc;
-            if (nm) bytes += 48.0 * L.Mown();
-            const double cbytes = 8.0 * ((zero ? 4.0 : 5.0) * L.Mown() -
-                                         (vgu ? 2.0 * L.Mown() : 0.0) +
+            // points of the launched rows: the owned ones, or with the
+            // communication-avoiding extension the kPostExt rows past each end
+            const double M = double(A.rb - A.ra) * double(L.n + 1);
+            double bytes = 40.0 * k * M;
+            const double Mc = M / 4;
+            if (pr) bytes += 32.0 * M + 8.0 * Mc;
+            if (rs) bytes += 40.0 * M + 24.0 * Mc;
+            if (nm) bytes += 48.0 * M;
+            const double cbytes = 8.0 * ((zero ? 4.0 : 5.0) * M - (vgu ? 2.0 * M : 0.0) +
                                          ((pr ? 1 : 0) + (rs ? 1 : 0)) * Mc);
             int blocks = 0;
             CHK(launch(c, pr ? MGX_K_PSMOOTH : MGX_K_GS, l, bytes, cbytes,
@@ -642,10 +715,17 @@ static int smooth(mgx_ctx *c, int l, bool prolong, bool restrict_, bool norm) {
 
 // rhs of level l+1 restricted (owned rows): refresh its ghosts, or gather it
 // into the replicated sub-contexts; u[l+1] = 0 for the coming coarse solve
-static int coarse_rhs_ready(mgx_ctx *c, int l) {
+// side (dist_overlap >= 1, the cross pass): a partitioned level's rhs ghosts
+// go on the side stream -- behind the norm's host round trip -- and the level's
+// next pass waits for them (take_rhs).
+static int coarse_rhs_ready(mgx_ctx *c, int l, bool side = false) {
     Dist *d = c->dist;
     if (l + 1 < d->la) {
-        CHK(xchg(c, l + 1, kRhs));
+        if (side && overlap_mode(d) != 0 && d->world > 1)
+            CHK(side_exchange(
+                c, {XF{l + 1, kRhs}}, [&] { d->rhs_pending[l + 1] = 1; }, d->ev_rhs[l + 1]));
+        else
+            CHK(xchg(c, l + 1, kRhs));
         for (auto &p : d->parts) p.lv[l + 1].zero = true;
         return MGX_OK;
     }
@@ -701,7 +781,7 @@ static void dist_drop_spec(mgx_ctx *c) {
 // always has (boundary strips, global bands), takes the two 16-row bands next
 // to the ghosts too, after the join (launch_xsmooth phases 1 and 2).
 // Outputs, u_pre / u_post / coarse rhs, are the same rows either way: bitwise.
-static int dist_cross(mgx_ctx *c, bool store_post) {
+static int dist_cross(mgx_ctx *c, bool store_post, bool norm) {
     Dist *d = c->dist;
     const int G = kGhostFine;
     const int k = c->opt.nsmooth;
@@ -818,7 +898,10 @@ static int dist_cross(mgx_ctx *c, bool store_post) {
         L.spec = bufs[i].second;
         L.zero = false;
     }
-    CHK(coarse_rhs_ready(c, 0));
+    // the norm first: its all-reduce and read-back are what the host waits
+    // for; the exchanges below run behind that round trip (dist_overlap)
+    if (norm) CHK(norm_issue(c));
+    CHK(coarse_rhs_ready(c, 0, /*side=*/true));
     // the next cycle's level-0 input is u_pre: its ghosts now, on the side
     // stream, behind the coarse levels (after the coarse rhs exchange, which
     // the next level needs first)
@@ -872,7 +955,7 @@ int dist_vcycle(mgx_ctx *c, double *norm, bool store_post) {
         // cross pass (mgx.hip:op_vcycle)
         for (int sh = 1; sh < c->opt.shape; ++sh) {
             CHK(coarse_cycle(c, 1));
-            CHK(dist_cross(c, /*store_post=*/false));
+            CHK(dist_cross(c, /*store_post=*/false, /*norm=*/false));
             for (auto &p : d->parts) {
                 p.lv[0].cur = p.lv[0].spec;
                 p.lv[0].spec = -1;
@@ -884,8 +967,8 @@ int dist_vcycle(mgx_ctx *c, double *norm, bool store_post) {
             dist_drop_spec(c);
             return reduce_norm(c, norm);
         }
-        CHK(dist_cross(c, store_post));
-        return reduce_norm(c, norm);
+        CHK(dist_cross(c, store_post, /*norm=*/true));
+        return norm_finish(c, norm);
     }
     dist_drop_spec(c);
     CHK(dist_level(c, 0, norm != nullptr));
@@ -955,6 +1038,17 @@ int dist_rhs_norm(mgx_ctx *c, double *res0) {
     }
     CHK(xchg(c, 0, kRhs));
     return reduce_norm(c, res0);
+}
+
+// mgx_velocity_factored of a partitioned context: its first part's levels
+int dist_velocity_mask(mgx_ctx *c) {
+    Dist *d = c->dist;
+    if (d->parts.empty() || d->parts[0].lv.empty()) return 0;
+    const Part &p = d->parts[0];
+    int f = p.lv[0].sa1 ? 1 : 0;
+    for (size_t l = 1; l < p.lv.size() && l < 31; ++l)
+        if (p.lv[l].vgen && g_vgen) f |= 1 << l;
+    return f;
 }
 
 int dist_nsub(mgx_ctx *c) { return c->dist ? (int)c->dist->parts.size() : 0; }
@@ -1093,8 +1187,16 @@ int dist_download(mgx_ctx *c, double *u, hipMemcpyKind kind) {
     double *full = nullptr;
     HIPCHK(hipMalloc(&full, sizeof(double) * (size_t)(n + 1) * P));
     int rc = MGX_OK;
-    ncclResult_t r1 = ncclAllGather(L.U() + (long)L.ra * P, full, (size_t)q * P, ncclDouble,
-                                    d->comm, c->stream);
+    ncclResult_t r1 = ncclSuccess;
+    rc = comm_op(d, c->stream, [&]() -> int {
+        r1 = ncclAllGather(L.U() + (long)L.ra * P, full, (size_t)q * P, ncclDouble, d->comm,
+                           c->stream);
+        return MGX_OK;
+    });
+    if (rc) {
+        (void)hipFree(full);
+        return rc;
+    }
     // Drain before the next enqueue: with a size-1 communicator, RCCL 2.27's
     // all-gather followed directly by further stream work segfaulted on the
     // host (tests/test_gpu_dist.py::test_rccl_world1_equals_single).  The
@@ -1108,8 +1210,11 @@ int dist_download(mgx_ctx *c, double *u, hipMemcpyKind kind) {
         (void)hipMemcpyAsync(full + n * P, L.U() + n * P, sizeof(double) * P,
                              hipMemcpyDeviceToDevice, c->stream);
     if (r1 == ncclSuccess)
-        r1 = ncclBroadcast(full + n * P, full + n * P, (size_t)P, ncclDouble, d->world - 1,
-                           d->comm, c->stream);
+        rc = comm_op(d, c->stream, [&]() -> int {
+            r1 = ncclBroadcast(full + n * P, full + n * P, (size_t)P, ncclDouble, d->world - 1,
+                               d->comm, c->stream);
+            return MGX_OK;
+        });
     if (r1 != ncclSuccess) rc = fail(MGX_E_RCCL, ncclGetErrorString(r1));
     if (rc == MGX_OK &&
         (hipMemcpy2DAsync(u, row, full, P * sizeof(double), row, n + 1, kind, c->stream) ||
@@ -1157,6 +1262,66 @@ int dist_download_rows(mgx_ctx *c, int part, double *out, hipMemcpyKind kind) {
     return MGX_OK;
 }
 
+// Row-block upload, correct tower: which partitioned coarse levels generate
+// their velocity (PLevel::vgen) from the block's level-0 factors.  Level l's
+// entry (i, j) is the finest (2^l i, 2^l j); the generator reads the row
+// factor pair at finest row 2^l i, which for a coarse GHOST row lies outside
+// the rows this rank factored -- its pair is the level's own exchanged entry
+// in column j*/2^l (the finest row factors are the entries of column j*,
+// where the column factor is exactly 1: sepvel.h), so it is filled from
+// there.  Then every entry of every allocated row of the level is checked
+// bit for bit against the generator (k_vgen_check): a level whose rows do not
+// all match keeps reading its arrays.  Each rank decides for its own block.
+static int vgen_rows(mgx_ctx *c) {
+    Dist *d = c->dist;
+    for (auto &p : d->parts) {
+        PLevel &F = p.lv[0];
+        for (size_t l = 1; l < p.lv.size(); ++l) p.lv[l].vgen = false;
+        if (!p.vga || !F.sb1 || F.js1 < 0 || F.js2 < 0 || d->la < 2) continue;
+        // fill every level first (a later level rewrites rows of an earlier
+        // one with the same values on a consistent tower), then check
+        for (int l = 1; l < d->la; ++l) {
+            PLevel &L = p.lv[l];
+            const long m = (1L << l) - 1;
+            if ((F.js1 & m) || (F.js2 & m)) continue;
+            mgx::launch_vgen_fill_rows(p.vga, L.F(L.v1), L.F(L.v2), L.pitch, l,
+                                       (int)(F.js1 >> l), (int)(F.js2 >> l), L.lo, L.hi,
+                                       c->stream);
+            CHK(check_launch("vgen_fill_rows"));
+        }
+        int *dok = nullptr;
+        HIPCHK(hipMalloc(&dok, sizeof(int) * d->la));
+        std::vector<int> ok(d->la, 1);
+        int rc = hipMemcpyAsync(dok, ok.data(), sizeof(int) * d->la, hipMemcpyHostToDevice,
+                                c->stream) == hipSuccess ? MGX_OK : fail(MGX_E_HIP, "vgen_rows");
+        for (int l = 1; l < d->la && rc == MGX_OK; ++l) {
+            PLevel &L = p.lv[l];
+            mgx::VGen g;
+            g.a = p.vga;
+            g.b1 = F.sb1;
+            g.b2 = F.sb2;
+            g.l = l;
+            g.strided = 1;
+            mgx::launch_vgen_check(L.F(L.v1), L.F(L.v2), L.n, L.pitch, g, dok + l, c->stream,
+                                   L.lo, L.hi);
+            rc = check_launch("vgen_check (rows)");
+        }
+        if (rc == MGX_OK &&
+            (hipMemcpyAsync(ok.data(), dok, sizeof(int) * d->la, hipMemcpyDeviceToHost,
+                            c->stream) != hipSuccess ||
+             hipStreamSynchronize(c->stream) != hipSuccess))
+            rc = fail(MGX_E_HIP, "vgen_rows");
+        (void)hipFree(dok);
+        CHK(rc);
+        for (int l = 1; l < d->la; ++l) {
+            const long m = (1L << l) - 1;
+            p.lv[l].vgen = ok[l] == 1 && !(F.js1 & m) && !(F.js2 & m) && !(p.lv[l].n & 1) &&
+                           (p.lv[l].n << l) == c->N;
+        }
+    }
+    return MGX_OK;
+}
+
 // Row-block upload (no rank ever holds the whole grid): each part gets its
 // allocated rows [lo, hi] of u0 / v1 / v2 from the host, and the velocity
 // tower is built locally by injection (MGX_TOWER_CORRECT, each level from the
@@ -1187,20 +1352,35 @@ static int dist_upload_rows_impl(mgx_ctx *c, const double *const *u0s,
             L.spec = -1;
             L.zero = false;
             L.vz = 0x7fffffff;
-            L.vgen = false;   // (the correct tower is not the re-read it generates)
+            L.vgen = false;   // (set by vgen_rows once the tower is built)
         }
         PLevel &L = p.lv[0];
         const size_t row = w * sizeof(double), rows = L.hi - L.lo + 1;
         // velocity factors of this block's rows (every rank decides for its own
         // block: the factors only have to reproduce the rows its passes read)
         std::vector<double> a1, b1, a2, b2;
+        L.js1 = L.js2 = -1;
+        (void)hipFree(p.vga);
+        p.vga = nullptr;
         if (L.n >= kCrossMinN && c->L > 1 &&
             factor_velocity(v1s[i], v2s[i], c->N, L.lo, (long)rows, L.coef.h * 0.5, a1, b1, a2,
-                            b2))
+                            b2, &L.js1, &L.js2)) {
             CHK(part_factors(L, a1.data(), b1.data(), a2.data(), b2.data(), L.lo, (long)rows,
                              hipMemcpyHostToDevice, c->stream));
-        else
+            // the generator's row-factor pairs (VGen::a) of this block's rows;
+            // the coarse levels' ghost rows are added from their own exchanged
+            // rows below (vgen_rows)
+            std::vector<double2> h(rows);
+            for (size_t k = 0; k < rows; ++k) h[k] = make_double2(a1[k], a2[k]);
+            const size_t vb = sizeof(double2) * (size_t)(c->N + 2);
+            HIPCHK(hipMalloc(&p.vga, vb));
+            HIPCHK(hipMemsetAsync(p.vga, 0, vb, c->stream));
+            HIPCHK(hipMemcpyAsync(p.vga + L.lo, h.data(), sizeof(double2) * rows,
+                                  hipMemcpyHostToDevice, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));   // h goes out of scope
+        } else {
             drop_factors(L);
+        }
         HIPCHK(hipMemcpy2DAsync(L.u[0], L.pitch * sizeof(double), u0s[i], row, row, rows,
                                 hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipMemcpy2DAsync(L.v1, L.pitch * sizeof(double), v1s[i], row, row, rows,
@@ -1222,6 +1402,7 @@ static int dist_upload_rows_impl(mgx_ctx *c, const double *const *u0s,
         }
         CHK(xchg(c, {XF{l, kV1}, XF{l, kV2}}));
     }
+    CHK(vgen_rows(c));
     // first replicated level: owned rows into each sub-context, all-gathered
     const long nl = c->N >> d->la, q = nl / d->world;
     for (auto &p : d->parts) {
@@ -1259,8 +1440,11 @@ static int dist_upload_rows_impl(mgx_ctx *c, const double *const *u0s,
                 Part &p = d->parts[0];
                 Level &S = p.sub->lv[0];
                 double *a = f ? S.v2 : S.v1;
-                NCCLCHK(ncclAllGather(a + (long)p.rank * q * S.pitch, a, (size_t)q * S.pitch,
-                                      ncclDouble, d->comm, c->stream));
+                CHK(comm_op(d, c->stream, [&]() -> int {
+                    NCCLCHK(ncclAllGather(a + (long)p.rank * q * S.pitch, a, (size_t)q * S.pitch,
+                                          ncclDouble, d->comm, c->stream));
+                    return MGX_OK;
+                }));
             }
         }
     }
@@ -1388,15 +1572,9 @@ int mgx_create_dist(mgx_ctx **out, long n, int maxlvl, double dt, double nu,
             free_ctx(c);
             return fail(MGX_E_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
         }
-        // the side stream's communicator (collective: every rank splits here);
-        // without it (a split that fails on every rank alike) the context runs
-        // every exchange on the compute stream (overlap_mode 0)
-        r = ncclCommSplit(c->dist->comm, 0, rank, &c->dist->comm_x, nullptr);
-        if (r != ncclSuccess) {
-            c->dist->comm_x = nullptr;
-            fprintf(stderr, "mgx: ncclCommSplit failed (%s): every exchange stays on the "
-                            "compute stream\n", ncclGetErrorString(r));
-        }
+        // (one communicator: the side stream's exchanges use it too, chained
+        // after the compute stream's operations by comm_op -- no split
+        // communicator whose creation could fail on some ranks only)
     }
     int rc = build_dist(c, world, {rank});
     if (rc) {

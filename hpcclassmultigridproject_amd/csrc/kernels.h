@@ -75,17 +75,27 @@ enum : int { kModeZero = 1, kModeProlong = 2, kModeRestrict = 4, kModeNorm = 8 }
 // and the residual norm of uin against it goes to *norm_out -- a time step's
 // compute_rhs, mg_outer's initial norm and the first pre-smoothing in one pass.
 constexpr int kModeRhsNorm = 16;
-// Velocity generator of level l (1 or 2) of the reference tower (stencil.h
-// vg_col): its v1 / v2 entries from the finest level's exact factors
+// Velocity generator of level l (stencil.h vg_col): its v1 / v2 entries from
+// the finest level's exact factors -- level 1 or 2 of the reference tower
+// (strided 0: the injection quirk's re-read), or any level >= 1 of the correct
+// tower (strided 1: entry (i, j) = finest (2^l i, 2^l j))
 struct VGen {
     const double2 *a = nullptr;   // (sa1[I], sa2[I]), I = 0..N; (+0, +0) at N+1
     const double *b1 = nullptr, *b2 = nullptr;   // finest sb1, sb2 (0..N used)
     int l = 1;
+    int strided = 0;
 };
-// clear *ok (device int) unless every entry (i, j <= n) of level g.l's fields
-// v1, v2 (pitch) equals the generator's bits
+// clear *ok (device int) unless every entry (i in [r0, r1], j <= n) of level
+// g.l's fields v1, v2 (pitch; v + i*pitch = global row i) equals the
+// generator's bits; r1 < 0: every row 0..n
 void launch_vgen_check(const double *v1, const double *v2, long n, long pitch, VGen g, int *ok,
-                       hipStream_t s);
+                       hipStream_t s, int r0 = 0, int r1 = -1);
+// Row-block correct tower: a[i << l] = (v1(i, js1), v2(i, js2)) for rows
+// i in [r0, r1] of level l (the finest row factors are columns js << l of the
+// finest field, where the column factor is exactly 1: sepvel.h) -- the factors
+// of rows another rank factored, read from this rank's exchanged ghost rows
+void launch_vgen_fill_rows(double2 *a, const double *v1, const double *v2, long pitch, int l,
+                           int js1, int js2, int r0, int r1, hipStream_t s);
 struct SmoothArgs {
     const double *uin;
     double *uout;

@@ -144,22 +144,32 @@ __global__ __launch_bounds__(256) void k_row_nonzero(const double *v, long pitch
 // Level g.l entry (i = blockIdx.y, j) against the generator (stencil.h
 // vg_col): the same operands the wave march multiplies, compared bit for bit
 __global__ __launch_bounds__(256) void k_vgen_check(const double *v1, const double *v2, int n,
-                                                    long pitch, VGen g, int *ok) {
-    const int j = blockIdx.x * 256 + threadIdx.x, i = blockIdx.y, N = n << g.l;
+                                                    long pitch, VGen g, int *ok, int r0, int r1) {
+    const int j = blockIdx.x * 256 + threadIdx.x, N = n << g.l;
     if (j > n) return;
-    const VGCol k = vg_col(j, n, g.l);
-    const int st = vg_state(k, i), I = vg_row(k, i, st, g.l, N);
-    if (I < 0 || I > N + 1) {
-        *ok = 0;
-        return;
+    const VGCol k = vg_col(j, n, g.l, g.strided);
+    for (int i = r0 + (int)blockIdx.y; i <= r1; i += (int)gridDim.y) {
+        const int st = vg_state(k, i), I = vg_row(k, i, st, g.l, N);
+        if (I < 0 || I > N + 1) {
+            *ok = 0;
+            return;
+        }
+        const int c = st == 1 ? k.clo : k.chi;
+        const double2 a = g.a[I];
+        const double x = a.x * (st == 2 ? 0.0 : g.b1[c]), y = a.y * (st == 2 ? 0.0 : g.b2[c]);
+        const long o = (long)i * pitch + j;
+        if (__double_as_longlong(x) != __double_as_longlong(v1[o]) ||
+            __double_as_longlong(y) != __double_as_longlong(v2[o]))
+            *ok = 0;   // benign: every writer stores 0
     }
-    const int c = st == 1 ? k.clo : k.chi;
-    const double2 a = g.a[I];
-    const double x = a.x * (st == 2 ? 0.0 : g.b1[c]), y = a.y * (st == 2 ? 0.0 : g.b2[c]);
-    const long o = (long)i * pitch + j;
-    if (__double_as_longlong(x) != __double_as_longlong(v1[o]) ||
-        __double_as_longlong(y) != __double_as_longlong(v2[o]))
-        *ok = 0;   // benign: every writer stores 0
+}
+
+__global__ __launch_bounds__(256) void k_vgen_fill_rows(double2 *a, const double *v1,
+                                                        const double *v2, long pitch, int l,
+                                                        int js1, int js2, int r0, int r1) {
+    const int i = r0 + (int)(blockIdx.x * 256 + threadIdx.x);
+    if (i > r1) return;
+    a[(long)i << l] = make_double2(v1[(long)i * pitch + js1], v2[(long)i * pitch + js2]);
 }
 
 // Interior sum of squares, rows split over the grid; deterministic per block.
@@ -697,9 +707,22 @@ void launch_row_nonzero(const double *v, long pitch, long n, int *flags, hipStre
 }
 
 void launch_vgen_check(const double *v1, const double *v2, long n, long pitch, VGen g, int *ok,
-                       hipStream_t s) {
-    MGX_LAUNCH(k_vgen_check, dim3((unsigned)((n + 256) / 256), (unsigned)(n + 1)), dim3(256), s,
-               v1, v2, (int)n, pitch, g, ok);
+                       hipStream_t s, int r0, int r1) {
+    if (r1 < 0) {
+        r0 = 0;
+        r1 = (int)n;
+    }
+    if (r1 < r0) return;
+    const unsigned rows = (unsigned)std::min<long>(r1 - r0 + 1, 4096);
+    MGX_LAUNCH(k_vgen_check, dim3((unsigned)((n + 256) / 256), rows), dim3(256), s, v1, v2, (int)n,
+               pitch, g, ok, r0, r1);
+}
+
+void launch_vgen_fill_rows(double2 *a, const double *v1, const double *v2, long pitch, int l,
+                           int js1, int js2, int r0, int r1, hipStream_t s) {
+    if (r1 < r0) return;
+    MGX_LAUNCH(k_vgen_fill_rows, dim3((unsigned)((r1 - r0 + 256) / 256)), dim3(256), s, a, v1, v2,
+               pitch, l, js1, js2, r0, r1);
 }
 
 int norm_partials_size() { return kNormBlocks; }

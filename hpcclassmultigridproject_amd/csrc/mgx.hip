@@ -31,7 +31,7 @@ long g_sep_velocity = 1;
 
 bool factor_velocity(const double *v1, const double *v2, long n, long r0, long rows, double smin,
                      std::vector<double> &a1, std::vector<double> &b1, std::vector<double> &a2,
-                     std::vector<double> &b2) {
+                     std::vector<double> &b2, long *js1, long *js2) {
     (void)r0;
     if (!g_sep_velocity || !v1 || !v2 || rows < 1) return false;
     const long w = n + 1;
@@ -39,8 +39,8 @@ bool factor_velocity(const double *v1, const double *v2, long n, long r0, long r
     a2.assign(rows, 0.0);
     b1.assign(w, 0.0);
     b2.assign(w, 0.0);
-    return mgxsep::factor_rank1(v1, rows, w, w, smin, a1.data(), b1.data()) &&
-           mgxsep::factor_rank1(v2, rows, w, w, smin, a2.data(), b2.data());
+    return mgxsep::factor_rank1(v1, rows, w, w, smin, a1.data(), b1.data(), 0, js1) &&
+           mgxsep::factor_rank1(v2, rows, w, w, smin, a2.data(), b2.data(), 0, js2);
 }
 
 void free_level_factors(Level &L) {
@@ -137,10 +137,11 @@ int materialize(mgx_ctx *c, int l) {
 // last smoothing pass; *fused_norm tells the caller whether the norm was done.
 int op_prolong_add(mgx_ctx *c, int l);
 int op_restrict(mgx_ctx *c, int l);
-// tuning key "vgen": 1 (default) = levels 1-2 of the reference tower, when
-// their velocity passed the upload check (find_vgen), generate v1 / v2 in the
-// V-cycle's 3-sweep passes from the finest factors instead of reading them
-// (stencil.h vg_col; bitwise the same); 0 = reads them
+// tuning key "vgen": 1 (default) = levels 1-2 of the reference tower and
+// every coarse level of the correct tower, when their velocity passed the
+// upload check (find_vgen), generate v1 / v2 in the V-cycle's 3-sweep passes
+// from the finest factors instead of reading them (stencil.h vg_col; bitwise
+// the same); 0 = reads them
 long g_vgen = 1;
 static mgx::VGen level_vgen(const mgx_ctx *c, int l) {
     mgx::VGen g;
@@ -148,6 +149,7 @@ static mgx::VGen level_vgen(const mgx_ctx *c, int l) {
     g.b1 = c->lv[0].sb1;
     g.b2 = c->lv[0].sb2;
     g.l = l;
+    g.strided = c->opt.tower_mode == MGX_TOWER_CORRECT ? 1 : 0;
     return g;
 }
 int op_smooth(mgx_ctx *c, int l, int sweeps, bool prolong, bool restrict_, bool norm,
@@ -715,40 +717,44 @@ int find_zero_rows(mgx_ctx *c) {
     return rc;
 }
 
-// Levels 1-2 generate their velocity (Level::vgen) when the tower is the
-// reference's, the finest factors exist and every entry of the level equals
-// the generator's bits (k_vgen_check).  a1, a2: the finest row factors.
+// The coarse levels that generate their velocity (Level::vgen): levels 1-2 of
+// the reference tower (the injection quirk's closed form) or every level of
+// the correct tower (strided: the finest factors at rows / columns 2^l i,
+// 2^l j), below the coarsest (whose solve reads the arrays), when the finest
+// factors exist and every entry of the level equals the generator's bits
+// (k_vgen_check).  a1, a2: the finest row factors.
 int find_vgen(mgx_ctx *c, const std::vector<double> &a1, const std::vector<double> &a2) {
     for (auto &L : c->lv) L.vgen = false;
     (void)hipFree(c->vga);
     c->vga = nullptr;
     const Level &F = c->lv[0];
-    if (c->opt.tower_mode != MGX_TOWER_REFERENCE || !F.sa1 || c->L < 2 || (c->N & 3) ||
-        c->N > 32768 || (long)a1.size() != c->N + 1 || (long)a2.size() != c->N + 1)
+    const bool strided = c->opt.tower_mode == MGX_TOWER_CORRECT;
+    // (the reference closed form's integer products fit in int up to N = 2^15)
+    if (!F.sa1 || c->L < 3 || (c->N & 3) || (!strided && c->N > 32768) ||
+        (long)a1.size() != c->N + 1 || (long)a2.size() != c->N + 1)
         return MGX_OK;
     std::vector<double2> h((size_t)c->N + 2, make_double2(0.0, 0.0));
     for (long I = 0; I <= c->N; ++I) h[(size_t)I] = make_double2(a1[(size_t)I], a2[(size_t)I]);
     HIPCHK(hipMalloc(&c->vga, sizeof(double2) * h.size()));
+    const int top = strided ? c->L - 2 : std::min(c->L - 2, 2);
+    std::vector<int> ok(c->L, 0), one(c->L, 1);
     int *dok = nullptr;
-    HIPCHK(hipMalloc(&dok, sizeof(int) * 3));
-    const int top = std::min(c->L - 1, 2);
-    int ok[3] = {0, 0, 0}, one[3] = {1, 1, 1};
+    HIPCHK(hipMalloc(&dok, sizeof(int) * c->L));
     int rc = MGX_OK;
     if (hipMemcpyAsync(c->vga, h.data(), sizeof(double2) * h.size(), hipMemcpyHostToDevice,
                        c->stream) != hipSuccess ||
-        hipMemcpyAsync(dok, one, sizeof(one), hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        hipMemcpyAsync(dok, one.data(), sizeof(int) * c->L, hipMemcpyHostToDevice, c->stream) !=
+            hipSuccess)
         rc = fail(MGX_E_HIP, "find_vgen");
     for (int l = 1; l <= top && rc == MGX_OK; ++l) {
         const Level &L = c->lv[l];
-        if ((L.n << l) != c->N || (L.n & 1)) {
-            ok[l] = 0;
-            continue;
-        }
+        if ((L.n << l) != c->N || (L.n & 1)) continue;
         mgx::launch_vgen_check(L.v1, L.v2, L.n, L.pitch, level_vgen(c, l), dok + l, c->stream);
         rc = check_launch("vgen_check");
     }
     if (rc == MGX_OK &&
-        (hipMemcpyAsync(ok, dok, sizeof(ok), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        (hipMemcpyAsync(ok.data(), dok, sizeof(int) * c->L, hipMemcpyDeviceToHost, c->stream) !=
+             hipSuccess ||
          hipStreamSynchronize(c->stream) != hipSuccess))
         rc = fail(MGX_E_HIP, "find_vgen");
     (void)hipFree(dok);
@@ -1405,8 +1411,12 @@ extern "C" int mgx_factor_velocity(const double *v, long rows, long n, double sm
 // reads rhs and u only)
 extern "C" int mgx_velocity_factored(mgx_ctx *c, int *factored) {
     if (!c || !factored) return fail(MGX_E_ARG, "mgx_velocity_factored: bad args");
+    if (c->dist) {
+        *factored = dist_velocity_mask(c);
+        return MGX_OK;
+    }
     int f = (!c->lv.empty() && c->lv[0].sa1) ? 1 : 0;
-    for (size_t l = 1; l < c->lv.size() && l < 3; ++l)
+    for (size_t l = 1; l < c->lv.size() && l < 31; ++l)
         if (c->lv[l].vgen && mgxi::g_vgen) f |= 1 << l;
     *factored = f;
     return MGX_OK;
@@ -1432,6 +1442,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
     if (!strcmp(key, "dist_local_side")) {
         if (value != 0 && value != 1) return fail(MGX_E_ARG, "dist_local_side must be 0 or 1");
         mgxi::g_dist_local_side = value;
+        return MGX_OK;
+    }
+    if (!strcmp(key, "dist_comm_chain")) {   // test hook (dist.hip)
+        if (value != 0 && value != 1) return fail(MGX_E_ARG, "dist_comm_chain must be 0 or 1");
+        mgxi::g_dist_comm_chain = value;
         return MGX_OK;
     }
     if (!strcmp(key, "dist_min_rows")) {
@@ -1538,6 +1553,10 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "dist_local_side")) {
         *value = mgxi::g_dist_local_side;
+        return MGX_OK;
+    }
+    if (!strcmp(key, "dist_comm_chain")) {
+        *value = mgxi::g_dist_comm_chain;
         return MGX_OK;
     }
     if (!strcmp(key, "dist_min_rows")) {

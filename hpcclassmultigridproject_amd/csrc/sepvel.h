@@ -59,8 +59,9 @@ inline void parallel_rows(long rows, int nthreads, F &&f) {
 // v: rows x w, row-major (row stride ld).  On success a[rows], b[w] hold
 // exact factors.  smin: the smallest scaling (h/2 of the coarsest level that
 // uses the factors); 0 skips the range check.
+// jsel (optional): the column j* whose entries ARE the row factors (b_{j*} = 1).
 inline bool factor_rank1(const double *v, long rows, long w, long ld, double smin, double *a,
-                         double *b, int nthreads = 0) {
+                         double *b, int nthreads = 0, long *jsel = nullptr) {
     if (rows < 1 || w < 1) return false;
     const long cands[5] = {0, w / 2, w - 1, w / 4, (3 * w) / 4};
     constexpr int kC = 9;   // column-factor candidates: q and 4 neighbours each way
@@ -161,6 +162,7 @@ inline bool factor_rank1(const double *v, long rows, long w, long ld, double smi
             });
             if (!rng) return false;
         }
+        if (jsel) *jsel = js;
         return true;
     }
     return false;

@@ -203,12 +203,15 @@ struct RowData {
 // 1 (q = qh - 1) for rt <= i < rz, state 2 (zero) for i >= rz.  (VGen:
 // kernels.h; tests/test_vgen_formula.py checks the closed form against the
 // CPU checker's tower.)
+//
+// strided (MGX_TOWER_CORRECT, any level l >= 1): each level is the injection
+// of the one above, so entry (i, j) is the finest entry (2^l i, 2^l j) and
+// v1(i, j) = fl(sa1[2^l i] * sb1[2^l j]) -- one state (q = 0) on every row.
 struct VGCol {
     int qh, rt, rz, chi, clo;   // chi / clo: the finest column of states 0 / 1
 };
-__host__ __device__ inline VGCol vg_col(int j, int n, int l) {
+__host__ __device__ inline VGCol vg_col(int j, int n, int l, bool strided = false) {
     VGCol k;
-    const int N = n << l, W = N / 4 + 1, den = 2 * W - 1, s = 1 << (l - 1);
     if (j < 0 || j > n) {   // outside the level: every row zero
         k.qh = 0;
         k.rt = 0;
@@ -216,6 +219,13 @@ __host__ __device__ inline VGCol vg_col(int j, int n, int l) {
         k.chi = k.clo = 0;
         return k;
     }
+    if (strided) {
+        k.qh = 0;
+        k.rt = k.rz = 0x7fffffff;
+        k.chi = k.clo = j << l;
+        return k;
+    }
+    const int N = n << l, W = N / 4 + 1, den = 2 * W - 1, s = 1 << (l - 1);
     k.qh = s * j / W;
     k.rt = (s * j - k.qh * W) / s + 1;
     k.rz = (W * W - s * j + s * den - 1) / (s * den);

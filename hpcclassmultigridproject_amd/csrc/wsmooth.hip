@@ -95,7 +95,8 @@ struct WCfg {
 // the stages contract (four fmas), residuals
 // are d*(update - u); RHSN's rhs keeps the reference expressions (gs.cpp:44,
 // stored unscaled) and is scaled after.
-// VG: levels 1-2 of the reference tower, v1 / v2 generated from the finest
+// VG: levels 1-2 of the reference tower, or every level of the correct tower
+// (vg.strided), v1 / v2 generated from the finest
 // factors (stencil.h vg_col): per row two cached loads of the (sa1, sa2) pairs
 // of the lane's two columns replace the two HBM row loads; the lane's sb pairs
 // (three states per column) sit in its LDS slice and are multiplied in at the
@@ -150,8 +151,8 @@ __global__ __launch_bounds__(64 * WPB, (WCfg<K, MODE>::MINB)) void k_wsmooth(
         VGCol g0{}, g1{};
         const int lb = threadIdx.x * 6;
         if constexpr (VG) {   // (lane-private slice: no barrier)
-            g0 = vg_col(c0, n, vg.l);
-            g1 = vg_col(c0 + 1, n, vg.l);
+            g0 = vg_col(c0, n, vg.l, vg.strided);
+            g1 = vg_col(c0 + 1, n, vg.l, vg.strided);
             vgl[lb + 0] = make_double2(vg.b1[g0.chi], vg.b2[g0.chi]);
             vgl[lb + 1] = make_double2(vg.b1[g0.clo], vg.b2[g0.clo]);
             vgl[lb + 2] = make_double2(0.0, 0.0);

@@ -186,14 +186,19 @@ int mgx_synchronize(mgx_ctx *ctx);
  * "dist_min_rows": partitioned solvers replicate every level whose row blocks
  * would be shorter than this (default 256, even, >= 16); read at creation.
  * "dist_overlap": partitioned contexts, 1 = every partitioned level's u
- * ghost rows are exchanged on a second stream (and communicator) as soon as
- * the pass that wrote them ends, hidden behind the coarser levels (the
- * level's next pass waits for it); 2 = that, and the cross pass's remaining
- * exchange (level-1 u) on the
- * second stream beside the pass's interior march, the two 16-row bands next
+ * ghost rows are exchanged on a second stream as soon as the pass that wrote
+ * them ends, hidden behind the coarser levels (the level's next pass waits for
+ * it), and the cross pass's restricted level-1 rhs behind the norm's host
+ * round trip; 2 = that, and the cross pass's remaining exchange (level-1 u) on
+ * the second stream beside the pass's interior march, the two 16-row bands next
  * to the ghosts after it; 0 = every exchange on the compute stream; -1
  * (default) = 1 on an RCCL communicator, 0 on virtual ranks (one GPU, where
  * the side stream's copies compete with the passes).  Bitwise the same results.
+ * Whatever the mode, a rank has ONE communicator and at most one RCCL
+ * operation in flight: each is chained after the previous one by an event.
+ * "dist_comm_chain": test hook, 1 (default) = that chain; 0 drops it so the
+ * fake-RCCL test can show its happens-before check catching the overlap.
+ * Never 0 with real peers.
  * "dist_local_side": virtual ranks only: 0 (default) runs the dist_overlap
  * exchanges at their early points on the compute stream (one device: no
  * second link to overlap with), 1 on the second stream as over RCCL.  Bitwise
@@ -258,19 +263,31 @@ int mgx_set_tuning(const char *key, long value);
  * one L2-resident zero row instead of HBM; 0 = every row from HBM (bitwise
  * the same results).
  * "vgen": 1 (default) = levels 1-2 of the reference tower, whose v1 / v2 are
- * re-reads of the finest rank-1 field, generate them in the
- * V-cycle's 3-sweep smoothing passes from the finest level's factors instead
- * of reading them from HBM -- only when every entry of the level equals the
- * generator's bits (checked at upload, per level); 0 = reads them.  Bitwise
- * the same. */
+ * re-reads of the finest rank-1 field, and every level below the
+ * coarsest of the correct tower (strided injections of it: v_l(i, j) =
+ * fl(a[2^l i] * b[2^l j])), generate them in the V-cycle's 3-sweep smoothing
+ * passes from the finest level's factors instead of reading them from HBM --
+ * only when every entry of the level equals the generator's bits (checked at
+ * upload, per level; on row blocks per block, ghost rows included); 0 = reads
+ * them.  Bitwise the same. */
 /* Host only: exact rank-1 factors of v (rows x (n+1), row-major):
  * returns 1 and fills a[rows], b[n+1] with fl(a[i]*b[j]) == v[i][j] (same
  * bits) and every nonzero |v|, |b| still normal after scaling by smin, else 0. */
 int mgx_factor_velocity(const double *v, long rows, long n, double smin, double *a, double *b);
-/* *factored: bit 0 = the context keeps velocity factors for its finest level;
- * bits 1, 2 = level 1, 2 generates its velocity from them ("vgen"). */
+/* *factored: a bit mask (since round 4; before, 0 or 1 -- bit 0 keeps that
+ * meaning): bit 0 = the context keeps velocity factors for its finest level;
+ * bit l (l >= 1) = level l generates its velocity from them ("vgen": levels
+ * 1-2 of the reference tower, any level below the coarsest of the correct
+ * tower). */
 int mgx_velocity_factored(mgx_ctx *ctx, int *factored);
 int mgx_get_tuning(const char *key, long *value);
+/* Build provenance, fixed when the library was compiled: the sha256 (hex) of
+ * the kernel sources (csrc stencil.h, kernels.h, kernels.hip, wsmooth.hip,
+ * xsmooth.hip, concatenated in that order -- the key the committed PMC
+ * profiles are stamped with) and of every product source (those + ctx.h,
+ * plan.h, sepvel.h, mgx.hip, dist.hip, include/mgx.h). */
+const char *mgx_build_id(void);
+const char *mgx_build_sources_id(void);
 
 /* Per-kernel timing with HIP events on the context stream. */
 #define MGX_K_GS 0             /* RB-GS sweep (one full red+black sweep) */

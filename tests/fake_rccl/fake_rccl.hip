@@ -20,6 +20,17 @@
 //   * in-place all-gather (sendbuff == recvbuff + rank*count) and broadcast;
 //     any other overlap of send and receive buffers is rejected, as are
 //     buffers that run past the end of their device allocation.
+//   * one operation at a time per rank: NCCL operations of a communicator must
+//     not run concurrently (and those of two communicators may deadlock), so
+//     every operation a rank issues must be ORDERED after its previous one on
+//     the device -- the same stream, or an event chain.  A happens-before
+//     model checks that deterministically, whatever the timing: libmgx's
+//     hipEventRecord / hipStreamWaitEvent / hip*Synchronize calls are wrapped
+//     (-Wl,--wrap, tests/fake_rccl/Makefile) into vector clocks per stream,
+//     event and host thread; an operation on stream s whose clock does not
+//     cover the rank's previous operation is counted as a violation
+//     (fake_rccl_order_violations).  The fake's own event calls use the real
+//     functions, so peers never create the order a rank must create itself.
 // Data moves as device-to-device hipMemcpyAsync on the receiver's stream;
 // the all-reduce sums the ranks' values in rank order with a small kernel.
 // libmgx_fakerccl.so = libmgx's own objects + this file, linked -Bsymbolic
@@ -41,6 +52,16 @@
 #include <string>
 #include <vector>
 
+// libmgx's calls land in the __wrap_ functions below; the fake's own go
+// straight to the HIP runtime
+extern "C" {
+hipError_t __real_hipEventRecord(hipEvent_t e, hipStream_t s);
+hipError_t __real_hipStreamWaitEvent(hipStream_t s, hipEvent_t e, unsigned int flags);
+hipError_t __real_hipStreamSynchronize(hipStream_t s);
+hipError_t __real_hipEventSynchronize(hipEvent_t e);
+hipError_t __real_hipDeviceSynchronize(void);
+}
+
 namespace fk {
 
 enum Fn { kInit, kDestroy, kGroupStart, kGroupEnd, kSend, kRecv, kAllGather, kAllReduce,
@@ -61,6 +82,49 @@ ncclResult_t bad(ncclResult_t r, const std::string &msg) {
     fprintf(stderr, "fake_rccl: %s\n", msg.c_str());
     return r;
 }
+
+// ---- happens-before model (vector clocks) of the issuing threads' streams
+namespace hb {
+using VC = std::map<hipStream_t, long>;   // stream -> operations of it covered
+void join(VC &a, const VC &b) {
+    for (const auto &kv : b) {
+        long &x = a[kv.first];
+        if (kv.second > x) x = kv.second;
+    }
+}
+std::mutex mu;
+std::map<hipStream_t, VC> streams;   // what the work enqueued on a stream so far follows
+std::map<hipEvent_t, VC> events;     // the clock its last record captured
+thread_local VC host;                // what this host thread has synchronised with
+struct Last {
+    bool any = false;
+    hipStream_t st = nullptr;
+    long tick = 0;
+    std::string what;
+};
+thread_local Last last;   // this thread's (rank's) previous RCCL operation
+std::atomic<long> violations{0};
+std::string first;        // the first violation (under mu)
+
+// an RCCL operation of the calling rank issued on st
+void op(hipStream_t st, const char *what) {
+    std::lock_guard<std::mutex> g(mu);
+    VC &v = streams[st];
+    join(v, host);
+    if (last.any && last.st != st) {
+        const auto it = v.find(last.st);
+        const long seen = it == v.end() ? 0 : it->second;
+        if (seen < last.tick) {
+            if (violations++ == 0)
+                first = std::string(what) + " on stream " + std::to_string((uintptr_t)st) +
+                        " is not ordered after the rank's previous operation (" + last.what +
+                        " on stream " + std::to_string((uintptr_t)last.st) + ")";
+        }
+    }
+    const long t = ++v[st];
+    last = Last{true, st, t, what};
+}
+}  // namespace hb
 
 size_t type_size(ncclDataType_t t) {
     switch (t) {
@@ -167,8 +231,9 @@ ncclResult_t flush_group() {
     std::map<hipStream_t, hipEvent_t> ready;
     for (const Op &o : ops) {
         if (ready.count(o.st)) continue;
+        hb::op(o.st, "a send/recv group");
         hipEvent_t e = o.comm->event();
-        if (!e || hipEventRecord(e, o.st) != hipSuccess)
+        if (!e || __real_hipEventRecord(e, o.st) != hipSuccess)
             return bad(ncclUnhandledCudaError, "event record");
         ready[o.st] = e;
     }
@@ -206,7 +271,7 @@ ncclResult_t flush_group() {
             rc = bad(ncclInvalidUsage, "recv of " + std::to_string(o.bytes) + " B from rank " +
                                            std::to_string(o.peer) + " matched a send of " +
                                            std::to_string(p->bytes) + " B");
-        } else if (hipStreamWaitEvent(o.st, p->ready, 0) != hipSuccess ||
+        } else if (__real_hipStreamWaitEvent(o.st, p->ready, 0) != hipSuccess ||
                    hipMemcpyAsync(o.buf, p->src, o.bytes, hipMemcpyDeviceToDevice, o.st) !=
                        hipSuccess) {
             rc = bad(ncclUnhandledCudaError, "p2p copy");
@@ -217,7 +282,7 @@ ncclResult_t flush_group() {
     // 4. hand the completion back to the senders
     for (auto &kv : got) {
         hipEvent_t done = ops[0].comm->event();
-        if (!done || hipEventRecord(done, kv.first) != hipSuccess)
+        if (!done || __real_hipEventRecord(done, kv.first) != hipSuccess)
             rc = bad(ncclUnhandledCudaError, "event record");
         for (auto &qp : kv.second) {
             std::lock_guard<std::mutex> g(qp.first->mu);
@@ -237,7 +302,7 @@ ncclResult_t flush_group() {
             rc = bad(ncclInvalidUsage, "send of " + std::to_string(sp.second->bytes) +
                                            " B to rank " + std::to_string(sp.first->peer) +
                                            " did not match its receive");
-        if (sp.second->done && hipStreamWaitEvent(sp.first->st, sp.second->done, 0) != hipSuccess)
+        if (sp.second->done && __real_hipStreamWaitEvent(sp.first->st, sp.second->done, 0) != hipSuccess)
             rc = bad(ncclUnhandledCudaError, "stream wait");
     }
     return rc;
@@ -281,8 +346,10 @@ ncclResult_t collective(CollKind kind, const void *send, void *recv, size_t coun
     if (kind == kCollAllReduce && (t != ncclFloat64))
         return bad(ncclInvalidArgument, "all-reduce: only double sums are implemented");
     Clique &q = *comm->q;
+    hb::op(st, kind == kCollAllGather ? "an all-gather" : kind == kCollAllReduce ? "an all-reduce"
+                                                                                : "a broadcast");
     hipEvent_t ready = comm->event();
-    if (!ready || hipEventRecord(ready, st) != hipSuccess)
+    if (!ready || __real_hipEventRecord(ready, st) != hipSuccess)
         return bad(ncclUnhandledCudaError, "event record");
     const long seq = comm->seq++;
     std::shared_ptr<Coll> c;
@@ -316,7 +383,7 @@ ncclResult_t collective(CollKind kind, const void *send, void *recv, size_t coun
     // (2) reads on my stream
     double *stage = nullptr;
     auto cp = [&](void *dst, const void *src, size_t n, int from) {
-        if (hipStreamWaitEvent(st, c->ready[from], 0) != hipSuccess ||
+        if (__real_hipStreamWaitEvent(st, c->ready[from], 0) != hipSuccess ||
             hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, st) != hipSuccess)
             rc = bad(ncclUnhandledCudaError, "collective copy");
         g_bytes += (long)n;
@@ -337,7 +404,7 @@ ncclResult_t collective(CollKind kind, const void *send, void *recv, size_t coun
             // a persistent per-rank staging buffer, used in this rank's stream
             // order only (grown, with a device sync, for a larger count)
             if (comm->stage_bytes < bytes * R) {
-                (void)hipDeviceSynchronize();
+                (void)__real_hipDeviceSynchronize();
                 (void)hipFree(comm->stage);
                 comm->stage = nullptr;
                 comm->stage_bytes = 0;
@@ -352,7 +419,7 @@ ncclResult_t collective(CollKind kind, const void *send, void *recv, size_t coun
         }
     }
     hipEvent_t rd = comm->event();
-    if (!rd || hipEventRecord(rd, st) != hipSuccess) rc = bad(ncclUnhandledCudaError, "event");
+    if (!rd || __real_hipEventRecord(rd, st) != hipSuccess) rc = bad(ncclUnhandledCudaError, "event");
     {   // (3)
         std::unique_lock<std::mutex> g(q.mu);
         c->read_done[me] = rd;
@@ -361,7 +428,7 @@ ncclResult_t collective(CollKind kind, const void *send, void *recv, size_t coun
         q.cv.wait(g, [&] { return c->nread == R; });
     }
     for (int r = 0; r < R; ++r)
-        if (r != me && hipStreamWaitEvent(st, c->read_done[r], 0) != hipSuccess)
+        if (r != me && __real_hipStreamWaitEvent(st, c->read_done[r], 0) != hipSuccess)
             rc = bad(ncclUnhandledCudaError, "stream wait");
     // (4)
     if (kind == kCollAllReduce && stage && rc == ncclSuccess) {
@@ -439,7 +506,7 @@ static ncclResult_t init_rank(ncclComm_t *out, int nranks, const std::string &ke
         if (!warm) {
             hipLaunchKernelGGL(k_sum_ranks, dim3(1), dim3(256), 0, nullptr, c->stage, c->stage,
                                (size_t)0, 1);
-            if (hipDeviceSynchronize() != hipSuccess)
+            if (__real_hipDeviceSynchronize() != hipSuccess)
                 return bad(ncclUnhandledCudaError, "sum kernel warm-up");
             warm = true;
         }
@@ -477,7 +544,7 @@ ncclResult_t ncclCommDestroy(ncclComm_t c) {
     t_calls[kDestroy]++;
     if (!c) return ncclSuccess;
     for (hipEvent_t e : c->events) {
-        (void)hipEventSynchronize(e);
+        (void)__real_hipEventSynchronize(e);
         (void)hipEventDestroy(e);
     }
     (void)hipFree(c->stage);
@@ -547,7 +614,56 @@ ncclResult_t ncclBroadcast(const void *send, void *recv, size_t count, ncclDataT
     return collective(kCollBroadcast, send, recv, count, t, root, comm, st);
 }
 
+// ---- libmgx's stream-order calls (-Wl,--wrap): the happens-before model
+hipError_t __wrap_hipEventRecord(hipEvent_t e, hipStream_t s) {
+    {
+        std::lock_guard<std::mutex> g(hb::mu);
+        hb::VC &v = hb::streams[s];
+        hb::join(v, hb::host);
+        hb::events[e] = v;
+    }
+    return __real_hipEventRecord(e, s);
+}
+hipError_t __wrap_hipStreamWaitEvent(hipStream_t s, hipEvent_t e, unsigned int flags) {
+    {
+        std::lock_guard<std::mutex> g(hb::mu);
+        hb::VC &v = hb::streams[s];
+        hb::join(v, hb::host);
+        const auto it = hb::events.find(e);
+        if (it != hb::events.end()) hb::join(v, it->second);
+    }
+    return __real_hipStreamWaitEvent(s, e, flags);
+}
+hipError_t __wrap_hipStreamSynchronize(hipStream_t s) {
+    const hipError_t r = __real_hipStreamSynchronize(s);
+    std::lock_guard<std::mutex> g(hb::mu);
+    hb::join(hb::host, hb::streams[s]);
+    return r;
+}
+hipError_t __wrap_hipEventSynchronize(hipEvent_t e) {
+    const hipError_t r = __real_hipEventSynchronize(e);
+    std::lock_guard<std::mutex> g(hb::mu);
+    const auto it = hb::events.find(e);
+    if (it != hb::events.end()) hb::join(hb::host, it->second);
+    return r;
+}
+hipError_t __wrap_hipDeviceSynchronize(void) {
+    const hipError_t r = __real_hipDeviceSynchronize();
+    std::lock_guard<std::mutex> g(hb::mu);
+    for (const auto &kv : hb::streams) hb::join(hb::host, kv.second);
+    return r;
+}
+
 // ---- test hooks
+// RCCL operations (of any rank) issued while the rank's previous one was not
+// ordered before them, and the first such case
+long fake_rccl_order_violations(void) { return hb::violations.load(); }
+const char *fake_rccl_order_message(void) {
+    static thread_local std::string m;
+    std::lock_guard<std::mutex> g(hb::mu);
+    m = hb::first;
+    return m.c_str();
+}
 long fake_rccl_calls(const char *name) {
     for (int i = 0; i < kNumFn; ++i)
         if (!strcmp(name, kFnNames[i])) return g_calls[i].load();
@@ -567,6 +683,11 @@ const char *fake_rccl_error(void) {
 void fake_rccl_reset(void) {
     for (auto &c : g_calls) c = 0;
     g_bytes = 0;
+    hb::violations = 0;
+    {
+        std::lock_guard<std::mutex> g(hb::mu);
+        hb::first.clear();
+    }
     std::lock_guard<std::mutex> g(g_err_mu);
     g_err.clear();
 }

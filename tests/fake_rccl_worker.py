@@ -51,6 +51,8 @@ def fake():
     f.fake_rccl_bytes.restype = C.c_long
     f.fake_rccl_thread_calls.restype = C.c_long
     f.fake_rccl_thread_calls.argtypes = [C.c_char_p]
+    f.fake_rccl_order_violations.restype = C.c_long
+    f.fake_rccl_order_message.restype = C.c_char_p
     return f
 
 
@@ -95,6 +97,9 @@ def run_scenario(sc, ref_cache):
     dt = 1.0 / N / 10
     _lib.set_tuning("dist_min_rows", sc.get("min_rows", 256))
     _lib.set_tuning("dist_overlap", sc.get("overlap", 0))
+    # test hook: 0 drops dist.hip's RCCL operation chain (the negative case of
+    # the fake's happens-before check)
+    _lib.set_tuning("dist_comm_chain", sc.get("comm_chain", 1))
     fp = _lib.FP_FMA if sc.get("fp") == "fma" else _lib.FP_BITWISE
     u0, v1, v2 = init_problem(N)
     key = (N, L, tower, fp)
@@ -132,6 +137,7 @@ def run_scenario(sc, ref_cache):
         except Exception as e:   # noqa: BLE001 -- reported to the test
             errs[r] = f"{type(e).__name__}: {e}\n{traceback.format_exc()}"
 
+    viol0 = _FAKE.fake_rccl_order_violations()
     th = [threading.Thread(target=rank_main, args=(r,), daemon=True) for r in range(G)]
     t0 = time.time()
     for t in th:
@@ -142,8 +148,13 @@ def run_scenario(sc, ref_cache):
         # a rank died with peers blocked in a collective: report and bail out
         print(json.dumps({"hung": sc, "errors": errs}), flush=True)
         os._exit(3)
+    _lib.set_tuning("dist_comm_chain", 1)
     verdict = {"scenario": sc, "seconds": round(time.time() - t0, 2), "errors": errs,
-               "bitwise": {}, "norm_rel_err": 0.0, "steps_equal": True}
+               "bitwise": {}, "norm_rel_err": 0.0, "steps_equal": True,
+               # RCCL operations of a rank issued while its previous one was not
+               # ordered before them (fake_rccl.hip happens-before model)
+               "order_violations": _FAKE.fake_rccl_order_violations() - viol0,
+               "order_message": _FAKE.fake_rccl_order_message().decode()}
     if any(errs):
         return verdict
     W = N + 1

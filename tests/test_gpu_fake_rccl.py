@@ -11,7 +11,11 @@ with the cross-cycle pass, time steps, a plain V-cycle, whole-grid and
 row-block upload / download, with the finest exchange on the compute stream and
 overlapped on the second stream.  u must be bitwise the one-GPU context's,
 norms within 1e-11, cycle counts equal, and every NCCL call site of dist.hip
-must have run.
+must have run.  And no rank may ever have two RCCL operations in flight: the
+fake checks, with a happens-before model of libmgx's own event calls, that
+each operation is ordered after the rank's previous one (one communicator per
+rank, so none of two communicators either) -- and the scenario with that
+ordering switched off (test hook dist_comm_chain = 0) must be caught.
 """
 import json
 import os
@@ -48,6 +52,10 @@ def _scenarios():
     # fp_mode fma: bitwise the one-GPU fma context (partition-independent forms)
     sc.append(dict(N=4096, L=7, world=4, min_rows=16, overlap=1, fp="fma", full_download=True))
     sc.append(dict(N=16384, L=9, world=8, overlap=2, fp="fma"))
+    # the negative case: dist.hip's operation chain dropped (test hook) -- the
+    # side stream's early exchanges and the compute stream's collectives are
+    # then unordered, and the fake's happens-before check must say so
+    sc.append(dict(N=4096, L=7, world=4, min_rows=16, overlap=1, comm_chain=0))
     return sc
 
 
@@ -136,15 +144,18 @@ def test_rccl_branch_with_thread_peers_bitwise_vs_one_gpu(tmp_path):
             assert ph == v["ref_phase_xsmooth"], (sc, r, ph, v["ref_phase_xsmooth"])
         assert v["replicated_level"] >= 2, sc
         _assert_call_counts(v)
+        if sc.get("comm_chain", 1):
+            assert v["order_violations"] == 0, (sc, v["order_message"])
+        else:
+            assert v["order_violations"] > 0, ("unordered RCCL operations not caught", sc)
     # every NCCL call site of dist.hip ran: ghost send/recv in groups, the
     # in-place all-gathers (coarse rhs, download, row upload's velocity level),
     # the norm all-reduce, the download's broadcast
     calls = res["calls"]
     for name in ("ncclSend", "ncclRecv", "ncclGroupStart", "ncclGroupEnd", "ncclAllGather",
-                 "ncclAllReduce", "ncclBroadcast", "ncclCommInitRank", "ncclCommSplit",
-                 "ncclCommDestroy"):
+                 "ncclAllReduce", "ncclBroadcast", "ncclCommInitRank", "ncclCommDestroy"):
         assert calls[name] > 0, (name, calls)
     assert calls["ncclGroupStart"] == calls["ncclGroupEnd"]
-    # every context splits one side-stream communicator off its own
-    assert calls["ncclCommSplit"] == calls["ncclCommInitRank"]
-    assert calls["ncclCommDestroy"] == 2 * calls["ncclCommInitRank"]
+    # one communicator per context: the side stream's exchanges use it too
+    assert calls["ncclCommSplit"] == 0
+    assert calls["ncclCommDestroy"] == calls["ncclCommInitRank"]

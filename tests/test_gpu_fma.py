@@ -31,7 +31,14 @@ NORM_TOL = 1e-9
 
 
 def norm_floor(N):
-    return N * 1e-15
+    """Absolute floor of the norm comparison: the residual norm's rounding
+    floor.  Measured (round 4, 4 cycles): bitwise 7.3e-14 at N=16384 and
+    5.3e-15 at N=512, fma about 10x below (7.8e-16 at N=16384: one
+    subtraction of nearly equal numbers instead of a five-term sum), so once
+    a cycle reaches it the two modes differ by up to the bitwise floor.  1e-13
+    bounds cycles 3-4 at N=16384 (norms 2e-13 and 7e-14), where the round-4
+    floor N*1e-15 = 1.6e-11 left them unconstrained."""
+    return 1e-13
 
 
 @pytest.mark.parametrize("tag", ["N32", "N64", "N128", "N128_nu001"])

@@ -8,15 +8,17 @@ import os
 import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
-from bench import kernels_sha  # noqa: E402  (sha256 of the stencil kernel sources)
+from bench import kernels_sha, loaded_kernels_sha  # noqa: E402  (kernel sources sha256)
 
 src = json.load(open(sys.argv[1]))
 out = {"note": "rocprofv3 --pmc, one counter group per run (tools/pmc_collect.sh), "
                "N=16384 L=9, mean per dispatch; hbm_read_bytes = 2 x FETCH_SIZE KiB "
                "(gfx950 FETCH_SIZE counts half of a 16-B/lane streaming read, "
                "MI355X_MICROARCH.md HBM); hbm_write_bytes = WRITE_SIZE KiB",
-       # bench.py uses these bytes only while the kernel sources are unchanged
-       "kernel_sources_sha256": kernels_sha(),
+       # bench.py uses these bytes only with a library built from these kernel
+       # sources (mgx_build_id of the library that was profiled, = the tree's)
+       "kernel_sources_sha256": loaded_kernels_sha(),
+       "tree_kernel_sources_sha256": kernels_sha(),
        "mode": os.environ.get("MGX_PMC_MODE", "fma"),
        "kernels": {}}
 for k, v in src.items():
