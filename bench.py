@@ -167,6 +167,20 @@ def parse():
     return ap.parse_args()
 
 
+def velocity_note(mask, correct, L):
+    """How the run's passes get v1, v2 (mgx_velocity_factored bit mask)."""
+    if not mask:
+        return "2-D arrays on every level"
+    gen = [l for l in range(1, L) if mask >> l & 1]
+    s = "level 0: exact rank-1 factors (sep_velocity)"
+    if gen:
+        s += f"; levels {gen[0]}-{gen[-1]}: regenerated from them in the 3-sweep marches (vgen"
+        s += ", strided: the correct tower)" if correct else ", the reference tower's re-read)"
+    if not correct:
+        s += "; coarse levels: all-zero rows from one L2-resident row (zero_rows)"
+    return s + "; LDS-tile levels and the coarsest solve read the arrays"
+
+
 class Watchdog:
     """A deadline on a phase that waits on the other ranks (N > 1): an RCCL hang
     would otherwise stall the run silently until an outer time limit.  On
@@ -660,11 +674,8 @@ def main():
                    "last_residual": res},
         "roofline": roof,
         "kernels": kernels,
-        "velocity": ("level 0: exact rank-1 factors (sep_velocity); "
-                     + ("levels 1-2: regenerated from them (vgen); levels >= 3: "
-                        if fac.value & 6 else "coarse levels: ")
-                     + "all-zero rows from one L2-resident row (zero_rows)" if fac.value else
-                     "2-D arrays"),
+        "velocity": velocity_note(fac.value, tower == pkg._lib.TOWER_CORRECT, L)
+                    if world == 1 else None,
         "other_fp_mode": other,
         "generic_velocity_path": generic,
     }
