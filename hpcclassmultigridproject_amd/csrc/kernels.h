@@ -232,10 +232,11 @@ void launch_rhs_norm(double *rhs, const double *u, const double *v1, const doubl
 // Coarsest-level solve in one workgroup: repeat {GS; residual; norm} while
 // norm > tol and it < maxit (multigrid.cpp:58-65), in place on u.
 // zero_first: u = 0 before the first sweep.  stats[0] += iterations,
-// stats[1] = last norm.
+// stats[1] = last norm.  reps: the whole solve `reps` times in a row (a
+// W-cycle's `shape` visits of the coarsest level, multigrid.cpp:52) in one launch.
 void launch_coarse_solve(double *u, const double *rhs, const double *v1, const double *v2,
                          long n, long pitch, Coef c, double tol, int maxit, bool zero_first,
-                         double *stats, hipStream_t s);
+                         double *stats, hipStream_t s, int reps = 1);
 constexpr long kCoarseOneWgMaxN = 256;
 // 1 (default): coarsest levels n <= 64 solve with u, rhs, v1, v2 in LDS.
 void set_coarse_lds(long v);

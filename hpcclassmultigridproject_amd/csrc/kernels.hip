@@ -536,7 +536,7 @@ template <bool FM>
 __global__ __launch_bounds__(1024) void k_coarse_solve(double *u, const double *rhs,
                                                        const double *v1, const double *v2,
                                                        int n, long pitch, Coef c, double tol,
-                                                       int maxit, int zero_first,
+                                                       int maxit, int zero_first, int reps,
                                                        double *stats) {
     __shared__ double lds[16];
     __shared__ double s_norm;
@@ -549,8 +549,11 @@ __global__ __launch_bounds__(1024) void k_coarse_solve(double *u, const double *
         for (long p = t; p < (long)(n + 1) * pitch; p += 1024) u[p] = 0.0;
         __syncthreads();
     }
-    int it = 0;
+    int total = 0;
     double res = 1.0;
+    for (int rep = 0; rep < reps; ++rep) {
+    int it = 0;
+    res = 1.0;
     while (it < maxit && res > tol) {
         for (int colour = 0; colour < 2; ++colour) {
             for (int i = 1 + ty; i <= n - 1; i += 16) {
@@ -583,8 +586,10 @@ __global__ __launch_bounds__(1024) void k_coarse_solve(double *u, const double *
         ++it;
         __syncthreads();
     }
+    total += it;
+    }
     if (t == 0) {
-        stats[0] += it;
+        stats[0] += total;
         stats[1] = res;
     }
 }
@@ -594,70 +599,135 @@ __global__ __launch_bounds__(1024) void k_coarse_solve(double *u, const double *
 // instead of L2 round trips.  Same sweep order, term order and reduction
 // order as k_coarse_solve, so u, the norms and the iteration count are
 // bitwise those of k_coarse_solve.
+//
+// Latency, not work, is the cost of this kernel (~4 K points): every loop is
+// unrolled to its fixed trip count for n <= 64 (rows ty + 16m, columns tx +
+// 64h) with guards, and each colour stage first loads the neighbours of all of
+// a thread's points and then stores the updates (points of one colour are
+// independent), so each phase waits for ONE round of loads instead of one per
+// row.  The residual sums keep k_coarse_solve's order (rows m ascending per
+// thread, then the wave butterfly, then the 16 waves in order).
+// reps: the solve repeated back to back (a W-cycle visits the coarsest level
+// `shape` times in a row, multigrid.cpp:52-65) in this one launch.
 constexpr int kCoarseLdsMaxN = 64;
 template <bool FM>
 __global__ __launch_bounds__(1024) void k_coarse_solve_lds(double *u, const double *rhs,
                                                            const double *v1, const double *v2,
                                                            int n, long pitch, Coef c, double tol,
-                                                           int maxit, int zero_first,
+                                                           int maxit, int zero_first, int reps,
                                                            double *stats) {
     constexpr int NP = kCoarseLdsMaxN + 1;
     constexpr int SZ = NP * NP;
+    constexpr int MR = (kCoarseLdsMaxN + 16) / 16;   // rows per thread: ty + 16m <= 64
     __shared__ double su[SZ], sr[SZ], sx[SZ], sy[SZ];
     __shared__ double lds[16];
     __shared__ double s_norm;
     const int t = threadIdx.x;
     const int tx = t & 63, ty = t >> 6;
-    if (zero_first)
-        for (long p = t; p < (long)(n + 1) * pitch; p += 1024) u[p] = 0.0;
-    for (int i = ty; i <= n; i += 16)
-        for (int j = tx; j <= n; j += 64) {
-            const long p = (long)i * pitch + j;
-            const int q = i * NP + j;
-            su[q] = zero_first ? 0.0 : u[p];
-            // (FM: f' = f/d and t = v*h/2, stencil.h)
-            sr[q] = FM ? rhs[p] * c.rdgs : rhs[p];
-            sx[q] = FM ? v1[p] * (c.h * 0.5) : v1[p];
-            sy[q] = FM ? v2[p] * (c.h * 0.5) : v2[p];
-        }
-    __syncthreads();
-    int it = 0;
-    double res = 1.0;
-    while (it < maxit && res > tol) {
-        for (int colour = 0; colour < 2; ++colour) {
-            for (int i = 1 + ty; i <= n - 1; i += 16) {
-                const int jc = 1 + ((i + 1 + colour) & 1);
-                for (int j = jc + 2 * tx; j <= n - 1; j += 128) {
-                    const int q = i * NP + j;
-                    su[q] = FM ? fm_upd_t(sr[q], sx[q], sy[q], su[q - NP], su[q - 1],
-                                          su[q + NP], su[q + 1], c)
-                               : gs_point(sr[q], sx[q], sy[q], su[q - NP], su[q - 1], su[q + NP],
-                                          su[q + 1], c);
+    {   // fill: every load of the thread in flight at once
+        double a[MR][2], b[MR][2], x[MR][2], y[MR][2];
+#pragma unroll
+        for (int m = 0; m < MR; ++m)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int i = ty + 16 * m, j = tx + 64 * h;
+                a[m][h] = b[m][h] = x[m][h] = y[m][h] = 0.0;
+                if (i <= n && j <= n) {
+                    const long p = (long)i * pitch + j;
+                    if (!zero_first) a[m][h] = u[p];
+                    b[m][h] = rhs[p];
+                    x[m][h] = v1[p];
+                    y[m][h] = v2[p];
                 }
             }
+#pragma unroll
+        for (int m = 0; m < MR; ++m)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int i = ty + 16 * m, j = tx + 64 * h;
+                if (i <= n && j <= n) {
+                    const int q = i * NP + j;
+                    su[q] = a[m][h];
+                    // (FM: f' = f/d and t = v*h/2, stencil.h)
+                    sr[q] = FM ? b[m][h] * c.rdgs : b[m][h];
+                    sx[q] = FM ? x[m][h] * (c.h * 0.5) : x[m][h];
+                    sy[q] = FM ? y[m][h] * (c.h * 0.5) : y[m][h];
+                }
+            }
+    }
+    if (zero_first)   // (the row padding, as the L2 version leaves it)
+        for (int i = ty; i <= n; i += 16)
+            for (int j = n + 1 + tx; j < pitch; j += 64) u[(long)i * pitch + j] = 0.0;
+    __syncthreads();
+    int total = 0;
+    double res = 1.0;
+    for (int rep = 0; rep < reps; ++rep) {
+        int it = 0;
+        res = 1.0;
+        while (it < maxit && res > tol) {
+            for (int colour = 0; colour < 2; ++colour) {
+                // this thread's points of the colour: rows 1 + ty + 16m, the
+                // colour's column jc + 2tx of each (one per row for n <= 64)
+                int qs[MR - 1];
+                bool on[MR - 1];
+                double nN[MR - 1], nW[MR - 1], nS[MR - 1], nE[MR - 1];
+#pragma unroll
+                for (int m = 0; m < MR - 1; ++m) {
+                    const int i = 1 + ty + 16 * m;
+                    const int jc = 1 + ((i + 1 + colour) & 1);
+                    const int j = jc + 2 * tx;
+                    on[m] = i <= n - 1 && j <= n - 1;
+                    qs[m] = on[m] ? i * NP + j : NP + 1;
+                    const int q = qs[m];
+                    nN[m] = su[q - NP];
+                    nW[m] = su[q - 1];
+                    nS[m] = su[q + NP];
+                    nE[m] = su[q + 1];
+                }
+#pragma unroll
+                for (int m = 0; m < MR - 1; ++m) {
+                    if (!on[m]) continue;
+                    const int q = qs[m];
+                    su[q] = FM ? fm_upd_t(sr[q], sx[q], sy[q], nN[m], nW[m], nS[m], nE[m], c)
+                               : gs_point(sr[q], sx[q], sy[q], nN[m], nW[m], nS[m], nE[m], c);
+                }
+                __syncthreads();
+            }
+            // residual (k_coarse_solve's order: rows ascending per thread)
+            double acc = 0.0;
+            {
+                double rr[MR - 1];
+#pragma unroll
+                for (int m = 0; m < MR - 1; ++m) {
+                    const int i = 1 + ty + 16 * m, j = 1 + tx;
+                    rr[m] = 0.0;
+                    if (i <= n - 1 && j <= n - 1) {
+                        const int q = i * NP + j;
+                        rr[m] = FM ? fm_res_t(sr[q], sx[q], sy[q], su[q], su[q - NP], su[q - 1],
+                                              su[q + NP], su[q + 1], c)
+                                   : res_point(sr[q], sx[q], sy[q], su[q], su[q - NP],
+                                               su[q - 1], su[q + NP], su[q + 1], c);
+                    }
+                }
+#pragma unroll
+                for (int m = 0; m < MR - 1; ++m) {
+                    const int i = 1 + ty + 16 * m, j = 1 + tx;
+                    if (i <= n - 1 && j <= n - 1) acc += rr[m] * rr[m];
+                }
+            }
+            double s = block_sum(acc, lds);
+            if (t == 0) s_norm = sqrt(s);
+            __syncthreads();
+            res = s_norm;
+            ++it;
             __syncthreads();
         }
-        double acc = 0.0;
-        for (int i = 1 + ty; i <= n - 1; i += 16)
-            for (int j = 1 + tx; j <= n - 1; j += 64) {
-                const int q = i * NP + j;
-                const double r = FM ? fm_res_t(sr[q], sx[q], sy[q], su[q], su[q - NP], su[q - 1],
-                                               su[q + NP], su[q + 1], c)
-                                    : res_point(sr[q], sx[q], sy[q], su[q], su[q - NP],
-                                                su[q - 1], su[q + NP], su[q + 1], c);
-                acc += r * r;
-            }
-        double s = block_sum(acc, lds);
-        if (t == 0) s_norm = sqrt(s);
-        __syncthreads();
-        res = s_norm;
-        ++it;
-        __syncthreads();
+        total += it;
     }
-    for (int i = 1 + ty; i <= n - 1; i += 16)
-        for (int j = 1 + tx; j <= n - 1; j += 64) u[(long)i * pitch + j] = su[i * NP + j];
+    for (int i = ty; i <= n; i += 16)
+        for (int j = tx; j <= n; j += 64) u[(long)i * pitch + j] = su[i * NP + j];
     if (t == 0) {
-        stats[0] += it;
+        stats[0] += total;
         stats[1] = res;
     }
 }
@@ -934,23 +1004,23 @@ long get_coarse_lds() { return g_coarse_lds; }
 
 void launch_coarse_solve(double *u, const double *rhs, const double *v1, const double *v2,
                          long n, long pitch, Coef c, double tol, int maxit, bool zero_first,
-                         double *stats, hipStream_t s) {
+                         double *stats, hipStream_t s, int reps) {
     const int zf = zero_first ? 1 : 0;
     if (n <= kCoarseLdsMaxN && g_coarse_lds) {
         if (c.fm)
             MGX_LAUNCH(k_coarse_solve_lds<true>, dim3(1), dim3(1024), s, u, rhs, v1, v2, (int)n,
-                       pitch, c, tol, maxit, zf, stats);
+                       pitch, c, tol, maxit, zf, reps, stats);
         else
             MGX_LAUNCH(k_coarse_solve_lds<false>, dim3(1), dim3(1024), s, u, rhs, v1, v2, (int)n,
-                       pitch, c, tol, maxit, zf, stats);
+                       pitch, c, tol, maxit, zf, reps, stats);
         return;
     }
     if (c.fm)
         MGX_LAUNCH(k_coarse_solve<true>, dim3(1), dim3(1024), s, u, rhs, v1, v2, (int)n, pitch, c,
-                   tol, maxit, zf, stats);
+                   tol, maxit, zf, reps, stats);
     else
         MGX_LAUNCH(k_coarse_solve<false>, dim3(1), dim3(1024), s, u, rhs, v1, v2, (int)n, pitch, c,
-                   tol, maxit, zf, stats);
+                   tol, maxit, zf, reps, stats);
 }
 
 // ---------------------------------------------------------------- probes

@@ -290,31 +290,35 @@ int op_prolong_add(mgx_ctx *c, int l) {
     return MGX_OK;
 }
 
-// Coarsest level: GS until |r| <= coarse_tol or coarse_maxit (multigrid.cpp:55-65).
-int op_coarse(mgx_ctx *c, int l) {
+// Coarsest level: GS until |r| <= coarse_tol or coarse_maxit (multigrid.cpp:55-65),
+// `reps` times in a row (a W-cycle's `shape` visits, multigrid.cpp:52): one
+// launch for all of them when the level fits one workgroup.
+int op_coarse(mgx_ctx *c, int l, int reps) {
     Level &L = c->lv[l];
     if (L.n <= mgx::kCoarseOneWgMaxN) {
         const bool z = L.zero;
-        CHK(launch(c, MGX_K_COARSE, l, 88.0 * L.M(), 40.0 * L.M(), [&] {
+        CHK(launch(c, MGX_K_COARSE, l, 88.0 * L.M() * reps, 40.0 * L.M(), [&] {
             mgx::launch_coarse_solve(L.U(), L.rhs, L.v1, L.v2, L.n, L.pitch, L.coef,
                                      c->opt.coarse_tol, c->opt.coarse_maxit, z, c->dscal + 2,
-                                     c->stream);
+                                     c->stream, reps);
         }));
         L.zero = false;
         return MGX_OK;
     }
-    int it = 0;
-    double res = 1.0;
-    while (it < c->opt.coarse_maxit && res > c->opt.coarse_tol) {
-        bool fused = false;
-        CHK(op_smooth(c, l, 1, false, false, true, &fused));
-        if (fused)
-            CHK(read_norm(c, &res));
-        else
-            CHK(op_residual_norm(c, l, &res, 48.0));
-        ++it;
+    for (int r = 0; r < reps; ++r) {
+        int it = 0;
+        double res = 1.0;
+        while (it < c->opt.coarse_maxit && res > c->opt.coarse_tol) {
+            bool fused = false;
+            CHK(op_smooth(c, l, 1, false, false, true, &fused));
+            if (fused)
+                CHK(read_norm(c, &res));
+            else
+                CHK(op_residual_norm(c, l, &res, 48.0));
+            ++it;
+        }
+        c->hscal[4] += it;
     }
-    c->hscal[4] += it;
     return MGX_OK;
 }
 
@@ -448,10 +452,11 @@ int op_vcycle(mgx_ctx *c, int l, double *norm, bool store_post) {
     }
     if (l == 0) drop_spec(c);
     bool have_norm = false;
-    for (int sh = 0; sh < c->opt.shape; ++sh) {
+    // (the coarsest level's `shape` solves in a row: one op_coarse)
+    for (int sh = 0; sh < (l == c->L - 1 ? 1 : c->opt.shape); ++sh) {
         const bool last = sh == c->opt.shape - 1;
         if (l == c->L - 1) {
-            CHK(op_coarse(c, l));
+            CHK(op_coarse(c, l, c->opt.shape));
         } else {
             CHK(op_smooth(c, l, c->opt.nsmooth, false, /*restrict=*/true, false, nullptr));
             CHK(op_vcycle(c, l + 1));

@@ -732,8 +732,10 @@ static int smooth_winst(const SmoothArgs &A, hipStream_t s) {
     using C = WCfg<K, MODE>;
     MarchRegions inner, edge;
     march_regions<WPB>(A.n, C::W, C::H, A.ra, A.rb, C::TOP, C::BOT, false, inner, edge);
-    // the generated velocity: the V-cycle's 3-sweep pre / post passes
-    if constexpr (K == 3 && (MODE == (kModeZero | kModeRestrict) || MODE == kModeProlong))
+    // the generated velocity: the V-cycle's 3-sweep pre / post passes (and a
+    // W-cycle's second pre-smoothing of a visit, from a non-zero u)
+    if constexpr (K == 3 && (MODE == (kModeZero | kModeRestrict) || MODE == kModeProlong ||
+                             MODE == kModeRestrict))
         if (A.vg.a) return wsmooth_launch<WPB, K, MODE, true, true>(A, edge, A.partials,
                                                                      kNormBlocks / WPB, s);
     return wsmooth_launch<WPB, K, MODE, true>(A, edge, A.partials, kNormBlocks / WPB, s);
@@ -849,6 +851,7 @@ bool smooth_generates_velocity(const SmoothArgs &A0, int sweeps, int mode) {
     }
     if (mode == (kModeZero | kModeRestrict)) return !smooth_as_tiles<3, kModeZero | kModeRestrict>(A);
     if (mode == kModeProlong) return !smooth_as_tiles<3, kModeProlong>(A);
+    if (mode == kModeRestrict) return !smooth_as_tiles<3, kModeRestrict>(A);
     return false;
 }
 
