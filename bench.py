@@ -542,16 +542,20 @@ def main():
         r["kernel"] += f" = {kname}"
         r["traffic"] = traffic
         r["traffic_source"] = tsrc
-        # measured HBM bytes (rocprofv3 PMC, profiles/) / live mean duration
-        r["hbm_GBs"] = round(traffic / avg_s / 1e9, 1)
-        r["hbm_frac"] = round(traffic / avg_s / 1e9 / HBM_PEAK_GBS, 4)
         r["traffic_over_compulsory"] = round(traffic / per_launch, 3)
         # the profile's own kernel durations (rocprofv3, sum of the pass's
-        # launches): the live event mean should agree with them
+        # launches): the live event mean should agree with them.  The HBM
+        # rate is the profile's bytes over the profile's own durations (one
+        # box, one run), never the PMC bytes of one box over another's clock
         _, pms, _ = lookup_traffic(ids, mode, "ms_profiled")
         if pms:
             r["profiled_launch_ms"] = round(pms, 4)
             r["live_over_profiled"] = round(avg_s * 1e3 / pms, 4)
+            r["hbm_GBs"] = round(traffic / (pms * 1e-3) / 1e9, 1)
+            r["hbm_frac"] = round(r["hbm_GBs"] / HBM_PEAK_GBS, 4)
+            r["hbm_note"] = ("hbm_GBs = PMC bytes / rocprof duration of the same profile run "
+                             "(traffic_source); achieved = compulsory bytes / this run's live "
+                             "HIP-event mean")
         # VALU wave-instructions per launch (PMC SQ_INSTS_VALU, same profile)
         # against the issue capacity of the live duration (one wave64
         # instruction per 4 cycles per SIMD, 1024 SIMDs, 2.4 GHz peak clock:

@@ -125,6 +125,10 @@ struct SmoothArgs {
     int ra = 0, rb = -1, lo = 0, hi = -1;
 };
 int launch_smooth(const SmoothArgs &a, int sweeps, int mode, hipStream_t s);
+// A W-cycle's post-smoothing of one visit + pre-smoothing of the next on a tile
+// level as one pass (prolongation+add, 2 nsmooth sweeps, restriction); -1 if
+// the level marches or nsmooth is not 1..3.
+int launch_smooth_wpair(const SmoothArgs &a, int nsmooth, hipStream_t s);
 // whether launch_smooth(a, sweeps, mode) generates v1, v2 (a.vg, the 3-sweep
 // pre / post wave marches) instead of reading them: the launch's byte count
 bool smooth_generates_velocity(const SmoothArgs &a, int sweeps, int mode);

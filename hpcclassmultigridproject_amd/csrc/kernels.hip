@@ -594,19 +594,22 @@ __global__ __launch_bounds__(1024) void k_coarse_solve(double *u, const double *
     }
 }
 
-// The same solve with u, rhs, v1, v2 held in LDS (n <= 64: 4 x 65^2 doubles
-// = 135 KB of the CU's 160 KB): the loop's loads and stores are LDS accesses
-// instead of L2 round trips.  Same sweep order, term order and reduction
-// order as k_coarse_solve, so u, the norms and the iteration count are
-// bitwise those of k_coarse_solve.
+// The same solve with u held in LDS and each thread's rhs / v1 / v2 (FM: f',
+// t1, t2) in registers (n <= 64): the loop touches no global memory.  Same
+// sweep order, term order and reduction order as k_coarse_solve, so u, the
+// norms and the iteration count are bitwise those of k_coarse_solve.
 //
-// Latency, not work, is the cost of this kernel (~4 K points): every loop is
-// unrolled to its fixed trip count for n <= 64 (rows ty + 16m, columns tx +
-// 64h) with guards, and each colour stage first loads the neighbours of all of
-// a thread's points and then stores the updates (points of one colour are
-// independent), so each phase waits for ONE round of loads instead of one per
-// row.  The residual sums keep k_coarse_solve's order (rows m ascending per
-// thread, then the wave butterfly, then the 16 waves in order).
+// Latency and LDS issue, not work, are the cost of this kernel (~4 K points):
+//   * the colour stages map the 1024 threads onto the colour's points as
+//     (row 1 + (t >> 5) + 32p, the colour's column 2(t & 31) + 1 or + 2): two
+//     points per thread, every lane busy (k_coarse_solve's layout leaves half
+//     the lanes idle and gives the others four rows each), and each stage
+//     first reads the neighbours of both points, then stores both updates
+//     (the points of a colour are independent);
+//   * the residual keeps k_coarse_solve's layout (rows 1 + ty + 16m, column
+//     1 + tx) and its summation order (rows m ascending, then the wave
+//     butterfly, then the 16 waves in order), so the norms are its bits;
+//   * every loop is unrolled to its fixed trip count for n <= 64, guarded.
 // reps: the solve repeated back to back (a W-cycle visits the coarsest level
 // `shape` times in a row, multigrid.cpp:52-65) in this one launch.
 constexpr int kCoarseLdsMaxN = 64;
@@ -618,41 +621,66 @@ __global__ __launch_bounds__(1024) void k_coarse_solve_lds(double *u, const doub
                                                            double *stats) {
     constexpr int NP = kCoarseLdsMaxN + 1;
     constexpr int SZ = NP * NP;
-    constexpr int MR = (kCoarseLdsMaxN + 16) / 16;   // rows per thread: ty + 16m <= 64
-    __shared__ double su[SZ], sr[SZ], sx[SZ], sy[SZ];
+    constexpr int MR = kCoarseLdsMaxN / 16;   // residual rows per thread: 1 + ty + 16m <= 64
+    constexpr int GP = kCoarseLdsMaxN / 32;   // colour points per thread: rows 1 + r + 32p
+    __shared__ double su[SZ];
     __shared__ double lds[16];
     __shared__ double s_norm;
     const int t = threadIdx.x;
     const int tx = t & 63, ty = t >> 6;
-    {   // fill: every load of the thread in flight at once
-        double a[MR][2], b[MR][2], x[MR][2], y[MR][2];
+    const int gk = t & 31, gr = t >> 5;
+    const double hh = c.h * 0.5;
+    // per-point constants in registers: (f, t1, t2) = FM ? (rhs/d, v1*h/2, v2*h/2)
+    // : (rhs, v1, v2), exactly the operands the L2 version reads per use
+    auto consts = [&](long p, double &f, double &x, double &y) {
+        const double r = rhs[p], a = v1[p], b = v2[p];
+        f = FM ? r * c.rdgs : r;
+        x = FM ? a * hh : a;
+        y = FM ? b * hh : b;
+    };
+    double gf[2][GP], gx[2][GP], gy[2][GP];   // colour points
+    int gq[2][GP];
+    bool gon[2][GP];
+    double rf[MR], rx[MR], ry[MR];            // residual points
+    int rq[MR];
+    bool ron[MR];
 #pragma unroll
-        for (int m = 0; m < MR; ++m)
+    for (int colour = 0; colour < 2; ++colour)
+#pragma unroll
+        for (int p = 0; p < GP; ++p) {
+            const int i = 1 + gr + 32 * p;
+            const int j = 1 + ((i + 1 + colour) & 1) + 2 * gk;
+            gon[colour][p] = i <= n - 1 && j <= n - 1;
+            gq[colour][p] = gon[colour][p] ? i * NP + j : NP + 1;
+            gf[colour][p] = gx[colour][p] = gy[colour][p] = 0.0;
+            if (gon[colour][p])
+                consts((long)i * pitch + j, gf[colour][p], gx[colour][p], gy[colour][p]);
+        }
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+        const int i = 1 + ty + 16 * m, j = 1 + tx;
+        ron[m] = i <= n - 1 && j <= n - 1;
+        rq[m] = ron[m] ? i * NP + j : NP + 1;
+        rf[m] = rx[m] = ry[m] = 0.0;
+        if (ron[m]) consts((long)i * pitch + j, rf[m], rx[m], ry[m]);
+    }
+    {   // u into LDS: rows ty + 16m (m <= 4), columns tx, tx + 64, all loads in flight
+        constexpr int MF = (kCoarseLdsMaxN + 16) / 16;
+        double a[MF][2];
+#pragma unroll
+        for (int m = 0; m < MF; ++m)
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int i = ty + 16 * m, j = tx + 64 * h;
-                a[m][h] = b[m][h] = x[m][h] = y[m][h] = 0.0;
-                if (i <= n && j <= n) {
-                    const long p = (long)i * pitch + j;
-                    if (!zero_first) a[m][h] = u[p];
-                    b[m][h] = rhs[p];
-                    x[m][h] = v1[p];
-                    y[m][h] = v2[p];
-                }
+                a[m][h] = 0.0;
+                if (!zero_first && i <= n && j <= n) a[m][h] = u[(long)i * pitch + j];
             }
 #pragma unroll
-        for (int m = 0; m < MR; ++m)
+        for (int m = 0; m < MF; ++m)
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int i = ty + 16 * m, j = tx + 64 * h;
-                if (i <= n && j <= n) {
-                    const int q = i * NP + j;
-                    su[q] = a[m][h];
-                    // (FM: f' = f/d and t = v*h/2, stencil.h)
-                    sr[q] = FM ? b[m][h] * c.rdgs : b[m][h];
-                    sx[q] = FM ? x[m][h] * (c.h * 0.5) : x[m][h];
-                    sy[q] = FM ? y[m][h] * (c.h * 0.5) : y[m][h];
-                }
+                if (i <= n && j <= n) su[i * NP + j] = a[m][h];
             }
     }
     if (zero_first)   // (the row padding, as the L2 version leaves it)
@@ -665,55 +693,42 @@ __global__ __launch_bounds__(1024) void k_coarse_solve_lds(double *u, const doub
         int it = 0;
         res = 1.0;
         while (it < maxit && res > tol) {
-            for (int colour = 0; colour < 2; ++colour) {
-                // this thread's points of the colour: rows 1 + ty + 16m, the
-                // colour's column jc + 2tx of each (one per row for n <= 64)
-                int qs[MR - 1];
-                bool on[MR - 1];
-                double nN[MR - 1], nW[MR - 1], nS[MR - 1], nE[MR - 1];
 #pragma unroll
-                for (int m = 0; m < MR - 1; ++m) {
-                    const int i = 1 + ty + 16 * m;
-                    const int jc = 1 + ((i + 1 + colour) & 1);
-                    const int j = jc + 2 * tx;
-                    on[m] = i <= n - 1 && j <= n - 1;
-                    qs[m] = on[m] ? i * NP + j : NP + 1;
-                    const int q = qs[m];
-                    nN[m] = su[q - NP];
-                    nW[m] = su[q - 1];
-                    nS[m] = su[q + NP];
-                    nE[m] = su[q + 1];
+            for (int colour = 0; colour < 2; ++colour) {
+                double nN[GP], nW[GP], nS[GP], nE[GP];
+#pragma unroll
+                for (int p = 0; p < GP; ++p) {
+                    const int q = gq[colour][p];
+                    nN[p] = su[q - NP];
+                    nW[p] = su[q - 1];
+                    nS[p] = su[q + NP];
+                    nE[p] = su[q + 1];
                 }
 #pragma unroll
-                for (int m = 0; m < MR - 1; ++m) {
-                    if (!on[m]) continue;
-                    const int q = qs[m];
-                    su[q] = FM ? fm_upd_t(sr[q], sx[q], sy[q], nN[m], nW[m], nS[m], nE[m], c)
-                               : gs_point(sr[q], sx[q], sy[q], nN[m], nW[m], nS[m], nE[m], c);
+                for (int p = 0; p < GP; ++p) {
+                    if (!gon[colour][p]) continue;
+                    su[gq[colour][p]] =
+                        FM ? fm_upd_t(gf[colour][p], gx[colour][p], gy[colour][p], nN[p], nW[p],
+                                      nS[p], nE[p], c)
+                           : gs_point(gf[colour][p], gx[colour][p], gy[colour][p], nN[p], nW[p],
+                                      nS[p], nE[p], c);
                 }
                 __syncthreads();
             }
-            // residual (k_coarse_solve's order: rows ascending per thread)
             double acc = 0.0;
             {
-                double rr[MR - 1];
+                double rr[MR];
 #pragma unroll
-                for (int m = 0; m < MR - 1; ++m) {
-                    const int i = 1 + ty + 16 * m, j = 1 + tx;
-                    rr[m] = 0.0;
-                    if (i <= n - 1 && j <= n - 1) {
-                        const int q = i * NP + j;
-                        rr[m] = FM ? fm_res_t(sr[q], sx[q], sy[q], su[q], su[q - NP], su[q - 1],
-                                              su[q + NP], su[q + 1], c)
-                                   : res_point(sr[q], sx[q], sy[q], su[q], su[q - NP],
-                                               su[q - 1], su[q + NP], su[q + 1], c);
-                    }
+                for (int m = 0; m < MR; ++m) {
+                    const int q = rq[m];
+                    rr[m] = FM ? fm_res_t(rf[m], rx[m], ry[m], su[q], su[q - NP], su[q - 1],
+                                          su[q + NP], su[q + 1], c)
+                               : res_point(rf[m], rx[m], ry[m], su[q], su[q - NP], su[q - 1],
+                                           su[q + NP], su[q + 1], c);
                 }
 #pragma unroll
-                for (int m = 0; m < MR - 1; ++m) {
-                    const int i = 1 + ty + 16 * m, j = 1 + tx;
-                    if (i <= n - 1 && j <= n - 1) acc += rr[m] * rr[m];
-                }
+                for (int m = 0; m < MR; ++m)
+                    if (ron[m]) acc += rr[m] * rr[m];
             }
             double s = block_sum(acc, lds);
             if (t == 0) s_norm = sqrt(s);

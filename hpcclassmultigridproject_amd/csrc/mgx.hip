@@ -290,6 +290,46 @@ int op_prolong_add(mgx_ctx *c, int l) {
     return MGX_OK;
 }
 
+// A W-cycle's post-smoothing of visit sh and pre-smoothing of visit sh+1 on
+// level l as one tile pass (launch_smooth_wpair): prolongation + add,
+// 2 nsmooth sweeps, residual restricted into rhs[l+1], u[l+1] = 0 -- bitwise
+// the two passes.  *done = false (nothing launched) where it does not apply.
+long g_wpair = 1;   // tuning key "wpair"
+int op_wpair(mgx_ctx *c, int l, bool *done) {
+    *done = false;
+    Level &L = c->lv[l], &Cl = c->lv[l + 1];
+    const int k = c->opt.nsmooth;
+    if (!g_wpair || c->opt.smoother != 0 || k < 1 || k > 3 || c->opt.fuse < k || L.zero ||
+        Cl.zero)
+        return MGX_OK;
+    mgx::SmoothArgs A{};
+    A.uin = L.u[L.cur];
+    A.uout = L.u[L.nxt()];
+    A.rhs = L.rhs;
+    A.v1 = L.v1;
+    A.v2 = L.v2;
+    A.n = L.n;
+    A.pitch = L.pitch;
+    A.c = L.coef;
+    A.uc = Cl.U();
+    A.rhsc = Cl.rhs;
+    A.pitchc = Cl.pitch;
+    A.partials = c->partials;
+    A.norm_out = c->dscal;
+    // post (prolong + add, k sweeps) + pre (k sweeps, restrict)
+    const double bytes = (32.0 + 40.0 * k) * L.M() + 8.0 * Cl.M() + (40.0 * k + 40.0) * L.M() +
+                         24.0 * Cl.M();
+    const double cbytes = 8.0 * (3.0 * L.M() + 2.0 * L.Mv() + 2.0 * Cl.M());
+    int blocks = 0;
+    CHK(launch(c, MGX_K_PSMOOTH, l, bytes, cbytes,
+               [&] { blocks = mgx::launch_smooth_wpair(A, k, c->stream); }));
+    if (blocks < 0) return MGX_OK;   // a march level: the two passes as usual
+    L.cur = L.nxt();
+    Cl.zero = true;
+    *done = true;
+    return MGX_OK;
+}
+
 // Coarsest level: GS until |r| <= coarse_tol or coarse_maxit (multigrid.cpp:55-65),
 // `reps` times in a row (a W-cycle's `shape` visits, multigrid.cpp:52): one
 // launch for all of them when the level fits one workgroup.
@@ -452,14 +492,27 @@ int op_vcycle(mgx_ctx *c, int l, double *norm, bool store_post) {
     }
     if (l == 0) drop_spec(c);
     bool have_norm = false;
+    bool pre_done = false;   // visit sh's pre-smoothing ran fused with sh-1's post
     // (the coarsest level's `shape` solves in a row: one op_coarse)
     for (int sh = 0; sh < (l == c->L - 1 ? 1 : c->opt.shape); ++sh) {
         const bool last = sh == c->opt.shape - 1;
         if (l == c->L - 1) {
             CHK(op_coarse(c, l, c->opt.shape));
         } else {
-            CHK(op_smooth(c, l, c->opt.nsmooth, false, /*restrict=*/true, false, nullptr));
+            if (!pre_done)
+                CHK(op_smooth(c, l, c->opt.nsmooth, false, /*restrict=*/true, false, nullptr));
+            pre_done = false;
             CHK(op_vcycle(c, l + 1));
+            // W-cycles: this visit's post- and the next visit's pre-smoothing
+            // back to back -- one tile pass where the level runs as tiles
+            if (!last) {
+                bool fused = false;
+                CHK(op_wpair(c, l, &fused));
+                if (fused) {
+                    pre_done = true;
+                    continue;
+                }
+            }
             CHK(op_smooth(c, l, c->opt.nsmooth, /*prolong=*/true, false, norm && last,
                           &have_norm));
         }
@@ -1449,6 +1502,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgxi::g_dist_local_side = value;
         return MGX_OK;
     }
+    if (!strcmp(key, "wpair")) {
+        if (value != 0 && value != 1) return fail(MGX_E_ARG, "wpair must be 0 or 1");
+        mgxi::g_wpair = value;
+        return MGX_OK;
+    }
     if (!strcmp(key, "dist_comm_chain")) {   // test hook (dist.hip)
         if (value != 0 && value != 1) return fail(MGX_E_ARG, "dist_comm_chain must be 0 or 1");
         mgxi::g_dist_comm_chain = value;
@@ -1562,6 +1620,10 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "dist_comm_chain")) {
         *value = mgxi::g_dist_comm_chain;
+        return MGX_OK;
+    }
+    if (!strcmp(key, "wpair")) {
+        *value = mgxi::g_wpair;
         return MGX_OK;
     }
     if (!strcmp(key, "dist_min_rows")) {

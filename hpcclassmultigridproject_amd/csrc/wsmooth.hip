@@ -855,6 +855,38 @@ bool smooth_generates_velocity(const SmoothArgs &A0, int sweeps, int mode) {
     return false;
 }
 
+// A W-cycle's two adjacent smoothing passes of one tile level (the post-
+// smoothing of visit sh and the pre-smoothing of visit sh+1, multigrid.cpp:
+// 52, 69-88: nothing runs between them) as ONE LDS-tile pass: prolongation +
+// add, 2*nsmooth sweeps, residual restricted -- the same operations in the same
+// order as the two passes, so bitwise their result; one launch and one
+// stage chain instead of two.  Tiles only (the small, latency-bound levels,
+// where the 2x wider halo costs nothing that matters): -1 when the level
+// would march, or for nsmooth outside 1..3.
+int launch_smooth_wpair(const SmoothArgs &A0, int nsmooth, hipStream_t s) {
+    SmoothArgs A = A0;
+    if (A.rb < 0) {
+        A.ra = 0;
+        A.rb = (int)A.n + 1;
+        A.lo = 0;
+        A.hi = (int)A.n;
+    }
+    if (A.ra & 1) return -1;
+    constexpr int M = kModeProlong | kModeRestrict;
+    switch (nsmooth) {
+        case 1:
+            if (!smooth_as_tiles<1, M>(A)) return -1;
+            return smooth_tile_rows<2, M, 16>(A, s);
+        case 2:
+            if (!smooth_as_tiles<2, M>(A)) return -1;
+            return smooth_tile_rows<4, M, 16>(A, s);
+        case 3:
+            if (!smooth_as_tiles<3, M>(A)) return -1;
+            return smooth_tile_rows<6, M, 16>(A, s);
+        default: return -1;
+    }
+}
+
 int launch_smooth(const SmoothArgs &A0, int sweeps, int mode, hipStream_t s) {
     SmoothArgs A = A0;
     if (A.rb < 0) {

@@ -244,8 +244,14 @@ int mgx_synchronize(mgx_ctx *ctx);
  * forms the next step's rhs, initial norm and first pre-smoothing, which the
  * next mgx_step starts from (any other call in between drops them); 0 = each
  * step starts with its own rhs + norm pass.
- * "coarse_lds": 1 (default) solves coarsest levels n <= 64 with the fields
- * in LDS, 0 = through L2 (bitwise the same).
+ * "coarse_lds": 1 (default) solves coarsest levels n <= 64 with u in LDS
+ * and each thread's rhs / v1 / v2 in registers, 0 = through L2 (bitwise the
+ * same).  A W-cycle's `shape` consecutive solves of the coarsest level run in
+ * one launch either way.
+ * "wpair": 1 (default) runs a W-cycle's post-smoothing of one visit and the
+ * pre-smoothing of the next visit of an LDS-tile level (nothing runs between
+ * them, multigrid.cpp:52) as one tile pass of 2 nsmooth sweeps; 0 = two
+ * passes (bitwise the same).
  * None of them changes a bit of u or a cycle count; residual norms taken by
  * a different kernel (cross_cycle, post_only, step_fuse) agree to 1e-11
  * relative (other reduction trees; a cycle count could differ only on a norm

@@ -183,15 +183,17 @@ def test_work_order_does_not_change_results(N, L, G, cross, knobs):
         np.testing.assert_allclose(n, n_ref, rtol=NORM_RTOL)
 
 
-@pytest.mark.parametrize("N,L", [(4096, 7), (1024, 6), (256, 4)], ids=["c64", "c32", "c32s"])
-def test_coarse_solve_in_lds_equals_l2_version(N, L, knobs):
-    """coarse_lds: the coarsest solve with its fields in LDS gives bitwise the
-    u, norms and coarse iteration counts of the L2 version."""
+@pytest.mark.parametrize("N,L,shape", [(4096, 7, 1), (1024, 6, 1), (256, 4, 1), (1024, 5, 2)],
+                         ids=["c64", "c32", "c32s", "c64w"])
+def test_coarse_solve_in_lds_equals_l2_version(N, L, shape, knobs):
+    """coarse_lds: the coarsest solve with u in LDS and its constants in
+    registers gives bitwise the u, norms and coarse iteration counts of the L2
+    version (W-cycles: both solves of a visit in one launch)."""
     out = []
     u0, v1, v2 = init_problem(N)
     for v in (0, 1):
         knobs(coarse_lds=v)
-        with Multigrid(N, L, 1.0 / N / 10, NU) as mg:
+        with Multigrid(N, L, 1.0 / N / 10, NU, shape=shape) as mg:
             mg.upload(u0, v1, v2)
             cyc = [mg.step(1e-6) for _ in range(2)]
             out.append((mg.download(), cyc, mg.coarse_iterations(), mg.residual_norm(0)))
@@ -255,6 +257,45 @@ def test_wcycle_cross_passes_equal_unfused(N, L, kw, cross):
     assert x_ref == 0 and x_x == 2 * 4
     assert np.array_equal(u_x, u_ref)
     np.testing.assert_allclose(n_x, n_ref, rtol=NORM_RTOL)
+
+
+@pytest.mark.parametrize("nsmooth", [1, 2, 3])
+@pytest.mark.parametrize("fp", [_lib.FP_BITWISE, _lib.FP_FMA], ids=["bitwise", "fma"])
+def test_wcycle_tile_pairs_equal_unfused_and_oracle(oracle_mod, knobs, nsmooth, fp):
+    """W-cycles on the LDS-tile levels: a visit's post-smoothing and the next
+    visit's pre-smoothing as ONE tile pass (tuning key wpair, 2 nsmooth sweeps
+    between the prolongation and the restriction) -- bitwise the two passes,
+    and (bitwise mode) the CPU checker's mg_inner, multigrid.cpp:17-92 with
+    shape 2.  The coarsest level's two solves per visit run in one launch."""
+    N, L = 2048, 6   # levels 1..4 tiles (n <= 1024), coarsest 64
+    out = {}
+    for w in (0, 1):
+        knobs(wpair=w)
+        u0, v1, v2 = init_problem(N)
+        with Multigrid(N, L, 1.0 / N / 10, NU, shape=2, nsmooth=nsmooth, fp_mode=fp) as mg:
+            mg.upload(u0, v1, v2)
+            mg.rhs()
+            mg.profile(True)
+            for _ in range(2):
+                mg.mg_inner()
+            launches = mg.profile_get(_lib.K_PSMOOTH)[0] + mg.profile_get(_lib.K_GS)[0]
+            coarse = mg.profile_get(_lib.K_COARSE)[0]
+            mg.profile(False)
+            out[w] = (mg.download(), launches, coarse, mg.coarse_iterations())
+    assert np.array_equal(out[1][0], out[0][0])
+    assert out[1][3] == out[0][3]                  # the same coarse iterations
+    assert out[1][1] < out[0][1], (out[0][1], out[1][1])
+    assert out[0][2] == out[1][2] == 2 * 2 ** (L - 1)   # one launch per coarsest visit
+    if fp == _lib.FP_BITWISE:
+        O = oracle_mod
+        O.set_threads(8)
+        dt = 1.0 / N / 10
+        u0, v1, v2 = init_problem(N)
+        t = O.Tower(u0, v1, v2, N, L)
+        O.compute_rhs(t.ufine, N, v1, v2, dt, NU, 1.0 / N, rhs=t.rhsfine)
+        for _ in range(2):
+            t.mg_inner(dt, NU, shape=2, nsmooth=nsmooth)
+        assert np.array_equal(out[1][0], t.ufine)
 
 
 def test_wcycle_cross_vs_oracle_and_partitioned(oracle_mod, cross):

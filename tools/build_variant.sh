@@ -16,6 +16,6 @@ wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Wl,--no-undefined \
     -o hpcclassmultigridproject_amd/libmgx_$NAME.so \
     $D/build/var_$NAME/kernels.o $D/build/var_$NAME/wsmooth.o $D/build/var_$NAME/xsmooth.o \
-    $D/build/mgx.o $D/build/dist.o -L/opt/rocm/lib -lamdhip64 -lrccl \
+    $D/build/mgx.o $D/build/dist.o $D/build/build_id.o -L/opt/rocm/lib -lamdhip64 -lrccl \
     -lpthread -Wl,-rpath,/opt/rocm/lib
 echo built hpcclassmultigridproject_amd/libmgx_$NAME.so
