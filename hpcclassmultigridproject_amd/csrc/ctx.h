@@ -185,6 +185,7 @@ int dist_nsub(mgx_ctx *c);
 mgx_ctx *dist_sub(mgx_ctx *c, int i);
 int dist_la(mgx_ctx *c);
 int dist_velocity_mask(mgx_ctx *c);   // mgx_velocity_factored of a partitioned context
+int dist_settle(mgx_ctx *c);   // join the side stream's exchanges into the compute stream
 // levels whose row blocks would be shorter than this are replicated (tuning
 // key "dist_min_rows", default 256)
 extern long g_dist_min_rows;

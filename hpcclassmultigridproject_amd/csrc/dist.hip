@@ -1040,6 +1040,12 @@ int dist_rhs_norm(mgx_ctx *c, double *res0) {
     return reduce_norm(c, res0);
 }
 
+// mgx_synchronize of a partitioned context: the side stream's pending
+// exchanges are joined into the compute stream first, so that once the host
+// has synchronised it, no RCCL operation of this rank is in flight (a caller's
+// own collectives -- torch.distributed's barrier in bench.py -- may follow).
+int dist_settle(mgx_ctx *c) { return settle(c); }
+
 // mgx_velocity_factored of a partitioned context: its first part's levels
 int dist_velocity_mask(mgx_ctx *c) {
     Dist *d = c->dist;

@@ -1260,6 +1260,9 @@ int mgx_stream(mgx_ctx *c, void **stream) {
 }
 int mgx_synchronize(mgx_ctx *c) {
     if (!c) return fail(MGX_E_ARG, "null ctx");
+    // (partitioned: the side stream's exchanges too -- no RCCL operation of
+    // the context is in flight when this returns)
+    if (c->dist) CHK(dist_settle(c));
     HIPCHK(hipStreamSynchronize(c->stream));
     return MGX_OK;
 }

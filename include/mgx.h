@@ -173,6 +173,9 @@ int mgx_download_level(mgx_ctx *ctx, int level, int field, double *out);
 int mgx_coarse_iterations(mgx_ctx *ctx, long *iters);
 /* The HIP stream (hipStream_t) the context launches on. */
 int mgx_stream(mgx_ctx *ctx, void **stream);
+/* Waits for all of the context's work; a partitioned context's side-stream
+ * exchanges included, so no RCCL operation of it is in flight on return (the
+ * caller's own collectives may follow). */
 int mgx_synchronize(mgx_ctx *ctx);
 
 /* Process-wide tuning knobs.  "tile_max_n": levels with n <= value run the

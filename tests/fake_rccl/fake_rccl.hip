@@ -655,6 +655,14 @@ hipError_t __wrap_hipDeviceSynchronize(void) {
 }
 
 // ---- test hooks
+// 1 if the calling thread (rank) has synchronised on the host with the end of
+// its last RCCL operation (none is in flight from its point of view)
+int fake_rccl_rank_idle(void) {
+    std::lock_guard<std::mutex> g(hb::mu);
+    if (!hb::last.any) return 1;
+    const auto it = hb::host.find(hb::last.st);
+    return it != hb::host.end() && it->second >= hb::last.tick ? 1 : 0;
+}
 // RCCL operations (of any rank) issued while the rank's previous one was not
 // ordered before them, and the first such case
 long fake_rccl_order_violations(void) { return hb::violations.load(); }

@@ -53,6 +53,7 @@ def fake():
     f.fake_rccl_thread_calls.argtypes = [C.c_char_p]
     f.fake_rccl_order_violations.restype = C.c_long
     f.fake_rccl_order_message.restype = C.c_char_p
+    f.fake_rccl_rank_idle.restype = C.c_int
     return f
 
 
@@ -60,7 +61,7 @@ def sequence(mg, full_download, upload, calls=None):
     """The calls every rank (and the one-GPU context) makes; -> results.
     Per phase: the cross-pass launches (K_XSMOOTH events of this context) and,
     when `calls` is given (a rank), the NCCL calls this rank made in it."""
-    out = {"phase_xsmooth": {}, "phase_calls": {}}
+    out = {"phase_xsmooth": {}, "phase_calls": {}, "idle_after_sync": []}
     upload(mg)
     mg.profile(True, finest_only=True)
 
@@ -70,6 +71,8 @@ def sequence(mg, full_download, upload, calls=None):
         mg.profile_reset()
         r = fn()
         mg.synchronize()
+        if calls:   # mgx_synchronize left no RCCL operation of this rank in flight
+            out["idle_after_sync"].append(bool(_FAKE.fake_rccl_rank_idle()))
         out["phase_xsmooth"][name] = mg.profile_get(_lib.K_XSMOOTH, 0)[0]
         if calls:
             c1 = calls()
@@ -180,6 +183,7 @@ def run_scenario(sc, ref_cache):
     # NCCL calls per phase of every rank (thread-local counters of the fake)
     verdict["phase_calls"] = [res[r]["phase_calls"] for r in range(G)]
     verdict["replicated_level"] = res[0]["la"]
+    verdict["idle_after_sync"] = all(all(res[r]["idle_after_sync"]) for r in range(G))
     return verdict
 
 

@@ -144,6 +144,9 @@ def test_rccl_branch_with_thread_peers_bitwise_vs_one_gpu(tmp_path):
             assert ph == v["ref_phase_xsmooth"], (sc, r, ph, v["ref_phase_xsmooth"])
         assert v["replicated_level"] >= 2, sc
         _assert_call_counts(v)
+        # after mgx_synchronize no RCCL operation of the rank is in flight
+        # (a caller's own collectives may follow: bench.py's barriers)
+        assert v["idle_after_sync"], sc
         if sc.get("comm_chain", 1):
             assert v["order_violations"] == 0, (sc, v["order_message"])
         else:
