@@ -75,10 +75,6 @@ enum : int { kModeZero = 1, kModeProlong = 2, kModeRestrict = 4, kModeNorm = 8 }
 // and the residual norm of uin against it goes to *norm_out -- a time step's
 // compute_rhs, mg_outer's initial norm and the first pre-smoothing in one pass.
 constexpr int kModeRhsNorm = 16;
-// Mode bit 32 (with kModeZero | kModeRestrict, sweeps 3, row march only): the
-// smoothed u is not stored -- the level's pre-smoothing when its post pass
-// recomputes it (launch_rsmooth)
-constexpr int kModeNoStore = 32;
 // Velocity generator of level l (stencil.h vg_col): its v1 / v2 entries from
 // the finest level's exact factors -- level 1 or 2 of the reference tower
 // (strided 0: the injection quirk's re-read), or any level >= 1 of the correct
@@ -172,18 +168,8 @@ struct XArgs {
     // count, no norm), phase 2 = the edge launch only, its partials written
     // after the first `partials_done` and the norm taken over both; 0 = both.
     int band = 0, phase = 0, partials_done = 0;
-    // 2-D velocity: rows >= vz of v1 and v2 are all zero, read from zrow (as
-    // SmoothArgs::zrow / vz)
-    const double *zrow = nullptr;
-    int vz = 0x7fffffff;
 };
 int launch_xsmooth(const XArgs &a, int sweeps, hipStream_t s);
-// A coarse level's post-smoothing that recomputes its pre-smoothing (k_xsmooth
-// REC, whole level, one GPU, sweeps 2-3): u_out = GS^K(GS^K(0; rhs) + P(uc)),
-// bitwise the pre pass (from zero) + the post pass, without the pre-smoothed u
-// in HBM.  Reads rhs (+ v1, v2 rows < vz unless a.sa1 ...) and uc, writes
-// a.upre.  Returns > 0, or -1 (unsupported).
-int launch_rsmooth(const XArgs &a, int sweeps, hipStream_t s);
 // whether launch_xsmooth supports rhs_next on a whole level of size n
 bool xstep_supported(long n);
 // Cross pass: 1 = interior strips run the unguarded march (default), 0 = all guarded.

@@ -290,95 +290,6 @@ int op_prolong_add(mgx_ctx *c, int l) {
     return MGX_OK;
 }
 
-// Recomputed pre-smoothing (launch_rsmooth, tuning key "rsmooth"): in a
-// V-cycle a level l >= 1 starts from u = 0 (multigrid.cpp:77), so its
-// pre-smoothed u is nsmooth sweeps from zero on rhs[l] alone.  The pre pass
-// then only restricts (kModeNoStore: no u written) and the post pass re-runs
-// those sweeps in its wave A before the prolongation and the post sweeps --
-// the level's u_pre never goes through HBM (one write and one read of the
-// level saved), bitwise the same u.  Levels that march (n >= rsmooth_min_n),
-// single-GPU contexts, V-cycles.
-long g_rsmooth = 1;            // tuning key "rsmooth"
-long g_rsmooth_min_n = 4096;   // tuning key "rsmooth_min_n"
-static bool rsmooth_ok(const mgx_ctx *c, int l) {
-    const Level &L = c->lv[l];
-    return g_rsmooth && l >= 1 && l + 1 < c->L && !c->dist && c->opt.smoother == 0 &&
-           c->opt.shape == 1 && (c->opt.nsmooth == 2 || c->opt.nsmooth == 3) &&
-           c->opt.fuse >= c->opt.nsmooth && L.zero && L.n >= g_rsmooth_min_n &&
-           L.coef.dgs > 0;
-}
-// the pre-smoothing from zero + restriction, u not stored
-static int op_pre_nostore(mgx_ctx *c, int l) {
-    Level &L = c->lv[l], &Cl = c->lv[l + 1];
-    const int k = c->opt.nsmooth;
-    const int mode = mgx::kModeZero | mgx::kModeRestrict | mgx::kModeNoStore;
-    mgx::SmoothArgs A{};
-    A.uin = L.u[L.cur];
-    A.uout = L.u[L.nxt()];
-    A.rhs = L.rhs;
-    A.v1 = L.v1;
-    A.v2 = L.v2;
-    A.zrow = c->zrow;
-    A.vz = L.vz;
-    if (L.vgen && g_vgen) A.vg = level_vgen(c, l);
-    A.n = L.n;
-    A.pitch = L.pitch;
-    A.c = L.coef;
-    A.uc = Cl.U();
-    A.rhsc = Cl.rhs;
-    A.pitchc = Cl.pitch;
-    A.partials = c->partials;
-    A.norm_out = c->dscal;
-    const bool vgu = mgx::smooth_generates_velocity(A, k, mode);
-    const double bytes = 40.0 * k * L.M() + 40.0 * L.M() + 24.0 * Cl.M();
-    const double cbytes = 8.0 * (L.M() + (vgu ? 0.0 : 2.0 * L.Mv()) + Cl.M());
-    int blocks = 0;
-    CHK(launch(c, MGX_K_GS, l, bytes, cbytes,
-               [&] { blocks = mgx::launch_smooth(A, k, mode, c->stream); }));
-    if (blocks < 0) return fail(MGX_E_ARG, "launch_smooth: no-store pre-smoothing");
-    Cl.zero = true;   // (L stays zero: its u_pre is recomputed by op_rsmooth)
-    return MGX_OK;
-}
-// prolongation + post-smoothing with the pre-smoothing recomputed
-static int op_rsmooth(mgx_ctx *c, int l) {
-    Level &L = c->lv[l], &Cl = c->lv[l + 1];
-    CHK(materialize(c, l + 1));
-    const int k = c->opt.nsmooth;
-    mgx::XArgs A;
-    A.uin = L.u[L.cur];   // (not read: the pass starts from zero)
-    A.upre = L.u[L.nxt()];
-    A.upost = A.upre;
-    A.rhs = L.rhs;
-    A.v1 = L.v1;
-    A.v2 = L.v2;
-    A.zrow = c->zrow;
-    A.vz = L.vz;
-    A.sa1 = L.sa1;
-    A.sb1 = L.sb1;
-    A.sa2 = L.sa2;
-    A.sb2 = L.sb2;
-    A.uc = Cl.U();
-    A.pitchc = Cl.pitch;
-    A.rhsc = Cl.rhs;
-    A.partials = c->partials;
-    A.norm_out = c->dscal;
-    A.n = L.n;
-    A.pitch = L.pitch;
-    A.c = L.coef;
-    A.store_post = false;
-    // canonical: the pre pass's sweeps + prolongation + the post pass;
-    // compulsory: rhs (+ v rows < vz unless factored), the coarse u, u written
-    const double bytes = 40.0 * k * L.M() + (32.0 + 40.0 * k) * L.M() + 8.0 * Cl.M();
-    const double cbytes = 8.0 * (2.0 * L.M() + (L.sa1 ? 0.0 : 2.0 * L.Mv()) + Cl.M());
-    int r = 0;
-    CHK(launch(c, MGX_K_PSMOOTH, l, bytes, cbytes,
-               [&] { r = mgx::launch_rsmooth(A, k, c->stream); }));
-    if (r < 0) return fail(MGX_E_ARG, "launch_rsmooth: unsupported");
-    L.cur = L.nxt();
-    L.zero = false;
-    return MGX_OK;
-}
-
 // A W-cycle's post-smoothing of visit sh and pre-smoothing of visit sh+1 on
 // level l as one tile pass (launch_smooth_wpair): prolongation + add,
 // 2 nsmooth sweeps, residual restricted into rhs[l+1], u[l+1] = 0 -- bitwise
@@ -587,10 +498,6 @@ int op_vcycle(mgx_ctx *c, int l, double *norm, bool store_post) {
         const bool last = sh == c->opt.shape - 1;
         if (l == c->L - 1) {
             CHK(op_coarse(c, l, c->opt.shape));
-        } else if (rsmooth_ok(c, l)) {   // (V-cycle: one visit)
-            CHK(op_pre_nostore(c, l));
-            CHK(op_vcycle(c, l + 1));
-            CHK(op_rsmooth(c, l));
         } else {
             if (!pre_done)
                 CHK(op_smooth(c, l, c->opt.nsmooth, false, /*restrict=*/true, false, nullptr));
@@ -1598,16 +1505,6 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgxi::g_dist_local_side = value;
         return MGX_OK;
     }
-    if (!strcmp(key, "rsmooth")) {
-        if (value != 0 && value != 1) return fail(MGX_E_ARG, "rsmooth must be 0 or 1");
-        mgxi::g_rsmooth = value;
-        return MGX_OK;
-    }
-    if (!strcmp(key, "rsmooth_min_n")) {
-        if (value < 64) return fail(MGX_E_ARG, "rsmooth_min_n must be >= 64");
-        mgxi::g_rsmooth_min_n = value;
-        return MGX_OK;
-    }
     if (!strcmp(key, "wpair")) {
         if (value != 0 && value != 1) return fail(MGX_E_ARG, "wpair must be 0 or 1");
         mgxi::g_wpair = value;
@@ -1730,14 +1627,6 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "wpair")) {
         *value = mgxi::g_wpair;
-        return MGX_OK;
-    }
-    if (!strcmp(key, "rsmooth")) {
-        *value = mgxi::g_rsmooth;
-        return MGX_OK;
-    }
-    if (!strcmp(key, "rsmooth_min_n")) {
-        *value = mgxi::g_rsmooth_min_n;
         return MGX_OK;
     }
     if (!strcmp(key, "dist_min_rows")) {

@@ -57,9 +57,6 @@ struct WCfg {
     // summed (mg_outer's initial norm, multigrid.cpp:104) -- a time step's
     // compute_rhs, initial norm and first pre-smoothing in one pass
     static constexpr bool RHSN = (MODE & 16) != 0;
-    // NOST: the smoothed u is not stored (the level's pre-smoothing when its
-    // post pass recomputes it: kModeNoStore)
-    static constexpr bool NOST = (MODE & 32) != 0;
     static constexpr int S = 2 * K;
     static constexpr int E = S + ((REST || NORM) ? 1 : 0);
     static constexpr int H = (E + 1) / 2;
@@ -422,7 +419,7 @@ __global__ __launch_bounds__(64 * WPB, (WCfg<K, MODE>::MINB)) void k_wsmooth(
                     }
                 }
                 // (3) row s+2-S is final
-                if (!C::NOST) {
+                {
                     const int ro = s + 2 - S;
                     st2_if(uout + rowoff(ro, ip), c0, rowin(ro) && keep,
                            ur[(p + 2 - S + 2 * NR) % NR]);
@@ -738,8 +735,7 @@ static int smooth_winst(const SmoothArgs &A, hipStream_t s) {
     // the generated velocity: the V-cycle's 3-sweep pre / post passes (and a
     // W-cycle's second pre-smoothing of a visit, from a non-zero u)
     if constexpr (K == 3 && (MODE == (kModeZero | kModeRestrict) || MODE == kModeProlong ||
-                             MODE == kModeRestrict ||
-                             MODE == (kModeZero | kModeRestrict | kModeNoStore)))
+                             MODE == kModeRestrict))
         if (A.vg.a) return wsmooth_launch<WPB, K, MODE, true, true>(A, edge, A.partials,
                                                                      kNormBlocks / WPB, s);
     return wsmooth_launch<WPB, K, MODE, true>(A, edge, A.partials, kNormBlocks / WPB, s);
@@ -842,9 +838,6 @@ static int smooth_k(const SmoothArgs &A, int mode, hipStream_t s) {
         case 9: return smooth_block<K, 9>(A, s);
         case 10: return smooth_block<K, 10>(A, s);
         case 20: return smooth_block<K, 20>(A, s);
-        // (no store: the march only -- the tiles always store)
-        case kModeZero | kModeRestrict | kModeNoStore:
-            return smooth_winst<4, K, kModeZero | kModeRestrict | kModeNoStore>(A, s);
         default: return -1;
     }
 }
@@ -859,7 +852,6 @@ bool smooth_generates_velocity(const SmoothArgs &A0, int sweeps, int mode) {
     if (mode == (kModeZero | kModeRestrict)) return !smooth_as_tiles<3, kModeZero | kModeRestrict>(A);
     if (mode == kModeProlong) return !smooth_as_tiles<3, kModeProlong>(A);
     if (mode == kModeRestrict) return !smooth_as_tiles<3, kModeRestrict>(A);
-    if (mode == (kModeZero | kModeRestrict | kModeNoStore)) return true;
     return false;
 }
 

@@ -93,31 +93,13 @@ struct XCfg {
 // exact (sepvel.h checks the range) -- from the lane's column factors, held
 // in registers for the whole march.
 //
-// REC = true (a coarse level's post-smoothing that RECOMPUTES its pre-smoothing,
-// launch_rsmooth): in a V-cycle a level below the finest starts from u = 0
-// (multigrid.cpp:77), so its pre-smoothed u is K sweeps from zero on its rhs
-// alone.  Instead of storing it (the pre pass) and reading it back (the post
-// pass), wave A re-runs those K zero-input sweeps (no u loads), adds the
-// prolongation of the coarse correction to each final row as it hands it to B
-// (multigrid.cpp:81-83), and B runs the K post-smoothing sweeps and stores the
-// result -- no norm, no restriction, no u_post.  The same operations on the
-// same operands as the pre pass + post pass: bitwise their result.  The pre
-// pass then only restricts (kModeNoStore).
-// (Its velocity: the level's own factors (SV: the correct tower's coarse
-// levels are strided copies of the finest factors, exact) or the 2-D arrays
-// with the reference tower's all-zero rows read from one L2-resident zero row
-// (vz).  The levels-1-2 generator of the wave march (VG) was built here too:
-// its per-lane row indices took the kernel from 2 to 1 wave per SIMD or to
-// 110-160 spilled VGPRs.)
-//
 // FM = true (fp_mode fma, stencil.h): each row's rhs enters the ring as f' =
 // f/d at its first use (A: the row's first stage, before the hand-off, so B
 // receives it scaled), the per-row coefficients are the m = -c/d of the
 // contracted update (one fma each), every update is four fmas and every
 // residual d*(update - u).  B's time-step rhs (RS) keeps the reference
 // expressions (gs.cpp:44, stored unscaled) and is scaled after.
-template <int WPB, int K, bool G, bool RS = false, bool SV = false, bool FM = false,
-          bool REC = false>
+template <int WPB, int K, bool G, bool RS = false, bool SV = false, bool FM = false>
 __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     const double *__restrict__ uin, double *__restrict__ upost, double *__restrict__ upre,
     const double *__restrict__ rhs, const double *__restrict__ v1, const double *__restrict__ v2,
@@ -126,8 +108,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     int lo, int hi, int store_post, double *__restrict__ rhs_next,
     double *__restrict__ partials2, const double *__restrict__ sa1,
     const double *__restrict__ sb1, const double *__restrict__ sa2,
-    const double *__restrict__ sb2, const double *__restrict__ zrow, int vz) {
-    static_assert(!REC || !RS, "the recompute pass: no step mode");
+    const double *__restrict__ sb2) {
     using X = XCfg<K>;
     constexpr int S = X::S, H = X::H, NR = X::NR, W = X::W, D = X::D, NU = X::NU,
                   NRD = X::NRD, EA = X::EA, EB = X::EB;
@@ -140,15 +121,10 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     // level 0 in three alternated rounds, 2 VGPRs spilled; XU 3 no change)
     constexpr int XRV = (FM && SV && !G && !RS) ? MGX_XRV + 1 : MGX_XRV;
     constexpr int XU = MGX_XU;
-    // REC: the coarse parents of a hand-off row XP steps ahead
-#ifndef MGX_XP
-#define MGX_XP 3
-#endif
-    constexpr int XP = MGX_XP;
     // A forms each row's coefficients once (MGX_XACOEF; B always does).  Not
     // in the guarded edge kernel: there it takes the kernel past 256 VGPRs
     // (one wave per SIMD), and the edge launch is latency bound
-    constexpr bool XACOEF = MGX_XACOEF != 0 && !G && !REC;
+    constexpr bool XACOEF = MGX_XACOEF != 0 && !G;
     static_assert(XU >= 1 && XU <= NR - 3, "u prefetch distance");
     // row s+XRV takes the ring slot of row s+XRV-NR, last used by A's norm of
     // row s+1-S
@@ -205,11 +181,10 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             rd[i].r = rd[i].x = rd[i].y = make_double2(0.0, 0.0);
         }
         // A: u row R + its coarse parents (odd = R's parity, compile-time:
-        // an even row needs only the coarse row below it); REC: the parents
-        // only (u = 0 in, the prolongation added at the hand-off)
+        // an even row needs only the coarse row below it)
         auto load_u = [&](int R, UPre &u, const bool odd) {
             const int Rc = min(max(R, lo), hi);
-            if (!REC) u.X = ld2u(uin + rowoff(Rc, ip), bcl);
+            u.X = ld2u(uin + rowoff(Rc, ip), bcl);
             const double *p0 = uc + rowoff(Rc >> 1, ipc);
             u.q00 = ld1u(p0, bjl);
             u.q01 = ld1u(p0, bjl1);
@@ -256,9 +231,8 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             if (SV) {   // (32-bit byte offsets: the scalar loads' SGPR-offset form)
                 ar1[q] = *reinterpret_cast<const double *>(rowb(sa1, (unsigned)Rc * 8u));
                 ar2[q] = *reinterpret_cast<const double *>(rowb(sa2, (unsigned)Rc * 8u));
-            } else {   // (rows >= vz: all zero, from the L2-resident zero row)
-                const bool z = Rc >= vz;
-                const double2 x = ld2((z ? zrow : v1 + o) + cl), y = ld2((z ? zrow : v2 + o) + cl);
+            } else {
+                const double2 x = ld2((v1 + o) + cl), y = ld2((v2 + o) + cl);
                 d.x = make_double2(x.x * hh, x.y * hh);
                 d.y = make_double2(y.x * hh, y.y * hh);
             }
@@ -287,20 +261,19 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             // per SIMD: spills); guarded stages are branches, never CSE'd
             Coef cg = c;
             if (!GS) asm volatile("" : "+s"(cg.nu));
-            if (!GS && FM) asm volatile("" : "+s"(cg.gn));   // (the fma forms' operand)
             // (the unguarded kernel only runs with d > 0: xsmooth_inst)
             if (cs == 0) {
                 const double uW = dpp_shr1(ur[iR].y);
                 if (!GS || (inr && in0))
                     ur[iR].x = FM ? fm_upd_t(d.r.x, d.x.x, d.y.x, ur[iN].x, uW, ur[iS].x,
-                                             ur[iR].y, cg)
+                                             ur[iR].y, c)
                                   : gs_point_t<!GS>(d.r.x, d.x.x, d.y.x, ur[iN].x, uW, ur[iS].x,
                                                     ur[iR].y, cg);
             } else {
                 const double uE = dpp_shl1(ur[iR].x);
                 if (!GS || (inr && in1))
                     ur[iR].y = FM ? fm_upd_t(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x, ur[iS].y,
-                                             uE, cg)
+                                             uE, c)
                                   : gs_point_t<!GS>(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x,
                                                     ur[iS].y, uE, cg);
             }
@@ -398,32 +371,21 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
         // waitcnt pass see A's pending loads on B's path and drain them)
         int it = 0;
         if (isA) {
-            if (REC) {   // u = 0 in; the parents of the first XP hand-off rows
 #pragma unroll
-                for (int d = 0; d < XP; ++d)
-                    load_u(s0 + 2 - S + d, up[(d + 2 - S + 2 * NR) % NR], d & 1);
-            } else {
-#pragma unroll
-                for (int d = 0; d < 3; ++d) {
-                    load_u(s0 + d, up[d], d & 1);
-                    ur[d] = make_u(s0 + d, up[d], d & 1);
-                }
-#pragma unroll
-                for (int d = 3; d < 3 + XU; ++d) load_u(s0 + d, up[d], d & 1);
+            for (int d = 0; d < 3; ++d) {
+                load_u(s0 + d, up[d], d & 1);
+                ur[d] = make_u(s0 + d, up[d], d & 1);
             }
+#pragma unroll
+            for (int d = 3; d < 3 + XU; ++d) load_u(s0 + d, up[d], d & 1);
 #pragma unroll
             for (int d = 1; d < XRV; ++d) load_rv(s0 + d, d);
             for (;;) {
 #pragma unroll
                 for (int p = 0; p < NR; ++p) {   // s == p (mod NR)
                     const int s = s0 + it + (p & 1);
-                    if (REC) {   // u row s+3 enters as 0; parents XP hand-offs ahead
-                        ur[(p + 3) % NR] = make_double2(0.0, 0.0);
-                        load_u(s + 2 - S + XP, up[(p + 2 - S + XP + 2 * NR) % NR], (p + XP) & 1);
-                    } else {
-                        ur[(p + 3) % NR] = make_u(s + 3, up[(p + 3) % NR], (p + 3) & 1);
-                        load_u(s + 3 + XU, up[(p + 3 + XU) % NR], (p + 3 + XU) & 1);   // XU ahead
-                    }
+                    ur[(p + 3) % NR] = make_u(s + 3, up[(p + 3) % NR], (p + 3) & 1);
+                    load_u(s + 3 + XU, up[(p + 3 + XU) % NR], (p + 3 + XU) & 1);   // XU ahead
                     first_use((p + 1) % NR);   // row s+1: first used by stage 0 below
                     if (XACOEF) {
                         // the row's four coefficients once (as B does), not in
@@ -445,19 +407,14 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                     }
                     {
                         const int ro = s + 2 - S;
-                        double2 uf = ur[(p + 2 - S + 2 * NR) % NR];
-                        if (REC) {   // u_pre + P(uc): the post pass's input row
-                            UPre &u = up[(p + 2 - S + 2 * NR) % NR];
-                            u.X = uf;
-                            uf = make_u(ro, u, p & 1);
-                        }
+                        const double2 uf = ur[(p + 2 - S + 2 * NR) % NR];
                         uring[pr][(p + 2 - S + 2 * NR) % NU][l] = uf;
-                        if (!REC) st2_ifu(upost + rowoff(ro, ip), c0, post && own(ro), uf);
+                        st2_ifu(upost + rowoff(ro, ip), c0, post && own(ro), uf);
                     }
                     // residual norm of u_post (multigrid.cpp:112-113), column c0 of
                     // row s+1-S (its neighbours are final now; B takes column c0+1:
                     // half each balances the pair's VALU work)
-                    if (!REC) {
+                    {
                         const int r = s + 1 - S;
                         const int iR = (p + 1 - S + 2 * NR) % NR;
                         const int iN = (p - S + 2 * NR) % NR;
@@ -505,7 +462,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                     // residual norm of u_post (multigrid.cpp:112-113) on row s+2,
                     // column c0+1 (A takes c0): rows s+1..s+3 are still untouched
                     // u_post here
-                    if (!REC) {
+                    {
                         const int r = s + 2;
                         const int iR = (q + 2) % NR, iN = (q + 1) % NR, iS = (q + 3) % NR;
                         const double uE = dpp_shl1(ur[iR].x);
@@ -563,7 +520,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         st2_ifu(upre + rowoff(ro, ip), c0, own(ro),
                                 ur[(q + 2 - S + 2 * NR) % NR]);
                     }
-                    if (!REC && ((q + 1 - S) & 1) == 0) {   // compile-time row parity
+                    if (((q + 1 - S) & 1) == 0) {   // compile-time row parity
                         // residual -> coarse rhs at the even-even points (:73-75)
                         const int r = s + 1 - S;
                         const int iR = (q + 1 - S + 2 * NR) % NR;
@@ -595,7 +552,6 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
         if (__builtin_amdgcn_readfirstlane(strip) >= 0)
             march(strip * W - 2 * H, strip * W, strip * W + W, a, b);
     }
-    if (REC) return;   // (no norm)
     const double tot = wave_sum(acc);   // one partial per wave (A: columns c0, B: c0+1)
     if (l == 0) partials[(long)blockIdx.x * 2 * WPB + wv] = tot;
     if (RS) {
@@ -851,15 +807,16 @@ long g_xfast = 1;   // unguarded interior march kernels (tuning key "xfast")
 void set_xfast(long v) { g_xfast = v; }
 long get_xfast() { return g_xfast; }
 
-template <int WPB, int K, bool G, bool RS, bool SV, bool FM, bool REC = false>
+template <int WPB, int K, bool G, bool RS, bool SV, bool FM>
 static int xsmooth_slots() {
     static int slots = 0;   // resident workgroups of this instantiation
     if (!slots) {
         int dev = 0, cus = 0, per = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per, k_xsmooth<WPB, K, G, RS, SV, FM, REC>, 128 * WPB, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per,
+                                                           k_xsmooth<WPB, K, G, RS, SV, FM>,
+                                                           128 * WPB, 0);
         slots = std::max(1, cus) * std::max(1, per);
     }
     return slots;
@@ -868,7 +825,7 @@ static int xsmooth_slots() {
 // One launch over `reg`; min_rows: the fewest rows per workgroup (each
 // workgroup's march pays a warm-up of ~EA + EB + D rows).  Returns the norm
 // partials written (grid * 2 * WPB: one per wave) at `partials`.
-template <int WPB, int K, bool G, bool RS, bool SV, bool FM, bool REC = false>
+template <int WPB, int K, bool G, bool RS, bool SV, bool FM>
 static int xsmooth_launch_sv(const XArgs &A, const MarchRegions &reg, double *partials, int lo,
                              int hi, long min_rows, long max_wgs, hipStream_t s) {
     const long total = reg.pre[reg.count];
@@ -876,16 +833,14 @@ static int xsmooth_launch_sv(const XArgs &A, const MarchRegions &reg, double *pa
     long upw;
     MarchRegions r;
     using X = XCfg<K>;
-    const unsigned grid =
-        plan_march(reg, WPB, xsmooth_slots<WPB, K, G, RS, SV, FM, REC>(), min_rows, max_wgs,
-                   X::EA + X::EB + X::D + X::NR / 2, upw, r);
+    const unsigned grid = plan_march(reg, WPB, xsmooth_slots<WPB, K, G, RS, SV, FM>(), min_rows,
+                                     max_wgs, X::EA + X::EB + X::D + X::NR / 2, upw, r);
     // RS: the second partials (the next step's initial norm) at the same
     // offsets, kNormBlocks further on
-    MGX_LAUNCH((k_xsmooth<WPB, K, G, RS, SV, FM, REC>), dim3(grid), dim3(128 * WPB), s,
-               A.uin, A.upost, A.upre, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials,
-               (int)A.n, A.pitch, r, upw, A.c, lo, hi, A.store_post ? 1 : 0, A.rhs_next,
-               RS ? partials + kNormBlocks : (double *)nullptr, A.sa1, A.sb1, A.sa2, A.sb2,
-               A.zrow ? A.zrow : A.v1, A.zrow ? A.vz : 0x7fffffff);
+    MGX_LAUNCH((k_xsmooth<WPB, K, G, RS, SV, FM>), dim3(grid), dim3(128 * WPB), s, A.uin,
+               A.upost, A.upre, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n,
+               A.pitch, r, upw, A.c, lo, hi, A.store_post ? 1 : 0, A.rhs_next,
+               RS ? partials + kNormBlocks : (double *)nullptr, A.sa1, A.sb1, A.sa2, A.sb2);
     return (int)grid * 2 * WPB;
 }
 // SV when the level's velocity factors are given (XArgs::sa1); FM = the
@@ -1062,47 +1017,6 @@ int launch_xsmooth(const XArgs &A, int sweeps, hipStream_t s) {
     if (blocks > 0 && A.rhs_next)   // the next step's initial norm
         launch_norm_final(A.partials + kNormBlocks, blocks, A.norm2_out, 1, s);
     return blocks;
-}
-
-// The recompute pass (k_xsmooth REC) over a whole level: the unguarded kernel
-// on the interior strips x rows [TOP, n+1-BOT) and the guarded one on the
-// rest, as the cross pass (the unguarded form needs d > 0, xfast on);
-// otherwise one guarded launch.  SV when the level has velocity factors.
-#ifndef MGX_RWPB
-#define MGX_RWPB 4
-#endif
-template <int WPB, int K, bool FM, bool SV>
-static int rsmooth_fv(const XArgs &A, hipStream_t s) {
-    using X = XCfg<K>;
-    const long n = A.n;
-    const int ra = 0, rb = (int)n + 1, lo = 0, hi = (int)n;
-    const bool split = g_xfast != 0 && A.c.dgs > 0;
-    MarchRegions inner, edge, unused;
-    march_regions<WPB>(n, X::W, X::H, ra, rb, X::TOP, X::BOT, split, inner, unused);
-    march_regions<1>(n, X::W, X::H, ra, rb, X::TOP, X::BOT, split, unused, edge);
-    if (xsmooth_launch_sv<WPB, K, false, false, SV, FM, true>(
-            A, inner, A.partials, lo, hi, A.min_rows, kNormBlocks / (2 * WPB) / 2, s) < 0)
-        return -1;
-    xsmooth_launch_sv<1, K, true, false, SV, FM, true>(
-        A, edge, A.partials, lo, hi, std::min(MGX_XEDGE_ROWS, A.min_rows), kNormBlocks / 2 / 2, s);
-    return 1;
-}
-template <int K>
-static int rsmooth_k(const XArgs &A, hipStream_t s) {
-    const bool sv = A.sa1 && A.sb1 && A.sa2 && A.sb2;
-    if (A.c.fm)
-        return sv ? rsmooth_fv<MGX_RWPB, K, true, true>(A, s)
-                  : rsmooth_fv<MGX_RWPB, K, true, false>(A, s);
-    return sv ? rsmooth_fv<MGX_RWPB, K, false, true>(A, s)
-              : rsmooth_fv<MGX_RWPB, K, false, false>(A, s);
-}
-int launch_rsmooth(const XArgs &A, int sweeps, hipStream_t s) {
-    if (A.rb >= 0) return -1;   // whole levels (one GPU) only
-    switch (sweeps) {
-        case 2: return rsmooth_k<2>(A, s);
-        case 3: return rsmooth_k<3>(A, s);
-        default: return -1;
-    }
 }
 
 bool xstep_supported(long n) {

@@ -251,12 +251,6 @@ int mgx_synchronize(mgx_ctx *ctx);
  * and each thread's rhs / v1 / v2 in registers, 0 = through L2 (bitwise the
  * same).  A W-cycle's `shape` consecutive solves of the coarsest level run in
  * one launch either way.
- * "rsmooth": 1 (default) lets a V-cycle's coarse level (one GPU, a row-march
- * level with n >= "rsmooth_min_n", default 4096; nsmooth 2-3) skip storing
- * its pre-smoothed u: the pre pass only restricts, and the post pass re-runs
- * the pre-smoothing sweeps from zero before the prolongation and its own
- * sweeps (one write and one read of the level saved); 0 = store and re-read
- * it.  Bitwise the same.
  * "wpair": 1 (default) runs a W-cycle's post-smoothing of one visit and the
  * pre-smoothing of the next visit of an LDS-tile level (nothing runs between
  * them, multigrid.cpp:52) as one tile pass of 2 nsmooth sweeps; 0 = two

@@ -259,45 +259,6 @@ def test_wcycle_cross_passes_equal_unfused(N, L, kw, cross):
     np.testing.assert_allclose(n_x, n_ref, rtol=NORM_RTOL)
 
 
-@pytest.mark.parametrize("N,L,kw,min_n", [
-    (16384, 9, {}, 4096),                                   # config 3: levels 1-2
-    (16384, 9, dict(fp_mode=_lib.FP_FMA), 4096),
-    (4096, 7, dict(nsmooth=2), 1024),                       # K = 2, levels 1-2 (2048, 1024)
-    (4096, 7, dict(fp_mode=_lib.FP_FMA, tower_mode=_lib.TOWER_CORRECT), 1024),
-    (2048, 6, dict(nu=0.01), 512),                          # nu > 0
-], ids=["N16384", "N16384fma", "N4096nu2", "N4096fma_correct", "N2048_nupos"])
-def test_recomputed_pre_smoothing_equals_stored(N, L, kw, min_n, knobs):
-    """rsmooth: a coarse level's pre pass only restricts and its post pass
-    recomputes the pre-smoothed u (k_xsmooth REC, wave A re-running the
-    sweeps from zero, multigrid.cpp:69-88) -- bitwise the stored schedule,
-    over cycles and time steps, and fewer bytes: the level's u_pre is never
-    written."""
-    kw = dict(kw)
-    nu = kw.pop("nu", NU)
-    knobs(rsmooth_min_n=min_n)
-    out = {}
-    for r in (0, 1):
-        knobs(rsmooth=r)
-        u0, v1, v2 = init_problem(N)
-        with Multigrid(N, L, 1.0 / N / 10, nu, **kw) as mg:
-            mg.upload(u0, v1, v2)
-            mg.rhs()
-            mg.profile(True)
-            norms = [mg.run_cycles(1) for _ in range(3)]
-            cb = sum(mg.profile_get_ex(k, 1)[3] for k in (_lib.K_GS, _lib.K_PSMOOTH))
-            mg.profile(False)
-            ua = mg.download()
-            cyc = [mg.step(1e-6) for _ in range(2)]
-            out[r] = (norms, ua, cyc, mg.download(), cb)
-    a, b = out[0], out[1]
-    assert np.array_equal(b[1], a[1]) and np.array_equal(b[3], a[3])
-    assert b[2] == a[2]
-    np.testing.assert_allclose(b[0], a[0], rtol=1e-11)
-    # level 1: the u_pre write and read (2 x 8 (n+1)^2 bytes) are gone
-    n1 = N // 2
-    assert b[4] < a[4] - 1.5 * 8 * (n1 + 1) ** 2 * 3, (a[4], b[4])
-
-
 @pytest.mark.parametrize("nsmooth", [1, 2, 3])
 @pytest.mark.parametrize("fp", [_lib.FP_BITWISE, _lib.FP_FMA], ids=["bitwise", "fma"])
 def test_wcycle_tile_pairs_equal_unfused_and_oracle(oracle_mod, knobs, nsmooth, fp):
