@@ -149,16 +149,21 @@ __global__ __launch_bounds__(64 * WPB, (WCfg<K, MODE>::MINB)) void k_wsmooth(
         const bool in0 = act && c0 >= 1 && c0 <= n - 1;
         const bool in1 = act && c0 + 1 <= n - 1;
         VGCol g0{}, g1{};
-        const int lb = threadIdx.x * 6;
+        // slot k of lane t at vgl[k * NT + t] (slot-major: the lanes of a
+        // wave read consecutive 16-B words; lane-major, stride 96 B, was an
+        // 8-way LDS bank conflict on every read -- 5 M conflict cycles per
+        // level-1 pass in the round-4 PMC profile)
+        constexpr int NT = 64 * WPB;
+        const int lb = threadIdx.x;
         if constexpr (VG) {   // (lane-private slice: no barrier)
             g0 = vg_col(c0, n, vg.l, vg.strided);
             g1 = vg_col(c0 + 1, n, vg.l, vg.strided);
-            vgl[lb + 0] = make_double2(vg.b1[g0.chi], vg.b2[g0.chi]);
-            vgl[lb + 1] = make_double2(vg.b1[g0.clo], vg.b2[g0.clo]);
-            vgl[lb + 2] = make_double2(0.0, 0.0);
-            vgl[lb + 3] = make_double2(vg.b1[g1.chi], vg.b2[g1.chi]);
-            vgl[lb + 4] = make_double2(vg.b1[g1.clo], vg.b2[g1.clo]);
-            vgl[lb + 5] = make_double2(0.0, 0.0);
+            vgl[lb + 0 * NT] = make_double2(vg.b1[g0.chi], vg.b2[g0.chi]);
+            vgl[lb + 1 * NT] = make_double2(vg.b1[g0.clo], vg.b2[g0.clo]);
+            vgl[lb + 2 * NT] = make_double2(0.0, 0.0);
+            vgl[lb + 3 * NT] = make_double2(vg.b1[g1.chi], vg.b2[g1.chi]);
+            vgl[lb + 4 * NT] = make_double2(vg.b1[g1.clo], vg.b2[g1.clo]);
+            vgl[lb + 5 * NT] = make_double2(0.0, 0.0);
         }
 
         struct UPre {
@@ -236,8 +241,8 @@ __global__ __launch_bounds__(64 * WPB, (WCfg<K, MODE>::MINB)) void k_wsmooth(
         auto scale_rv = [&](RowData &d, const int R) {
             if constexpr (VG) {   // v = fl(a * b) of row R's states
                 const int Rc = min(max(R, lo), hi);
-                const double2 b0 = vgl[lb + vg_state(g0, Rc)];
-                const double2 b1 = vgl[lb + 3 + vg_state(g1, Rc)];
+                const double2 b0 = vgl[lb + vg_state(g0, Rc) * NT];
+                const double2 b1 = vgl[lb + (3 + vg_state(g1, Rc)) * NT];
                 const double2 a0 = d.x, a1 = d.y;
                 d.x = make_double2(a0.x * b0.x, a1.x * b1.x);
                 d.y = make_double2(a0.y * b0.y, a1.y * b1.y);
