@@ -54,13 +54,13 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s HBM3E
 # fp_mode, for the PMC traffic summary committed under profiles/
 # (tools/profile_round.sh): the cross pass is two launches, the unguarded
 # interior kernel and the guarded edge kernel; their traffic is summed.
-# k_xsmooth<WPB, K, G, RS, SV, FM, F>
-KERNEL_IDS = {("fma", 8): ("mgx::k_xsmooth<4, 3, false, false, true, true, false>",
-                           "mgx::k_xsmooth<1, 3, true, false, true, true, false>"),
-              ("bitwise", 8): ("mgx::k_xsmooth<4, 3, false, false, true, false, false>",
-                               "mgx::k_xsmooth<1, 3, true, false, true, false, false>"),
-              ("fma-generic", 8): ("mgx::k_xsmooth<4, 3, false, false, false, true, false>",
-                                   "mgx::k_xsmooth<1, 3, true, false, false, true, false>")}
+# k_xsmooth<WPB, K, G, RS, SV, FM>
+KERNEL_IDS = {("fma", 8): ("mgx::k_xsmooth<4, 3, false, false, true, true>",
+                           "mgx::k_xsmooth<1, 3, true, false, true, true>"),
+              ("bitwise", 8): ("mgx::k_xsmooth<4, 3, false, false, true, false>",
+                               "mgx::k_xsmooth<1, 3, true, false, true, false>"),
+              ("fma-generic", 8): ("mgx::k_xsmooth<4, 3, false, false, false, true>",
+                                   "mgx::k_xsmooth<1, 3, true, false, false, true>")}
 CSRC = os.path.join(ROOT, "hpcclassmultigridproject_amd", "csrc")
 KERNEL_SOURCES = ("stencil.h", "kernels.h", "kernels.hip", "wsmooth.hip", "xsmooth.hip")
 

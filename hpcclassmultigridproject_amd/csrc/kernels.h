@@ -175,10 +175,6 @@ bool xstep_supported(long n);
 // Cross pass: 1 = interior strips run the unguarded march (default), 0 = all guarded.
 void set_xfast(long v);
 long get_xfast();
-// Whole-level cross pass as one launch (unguarded march with uniform row
-// tests and boundary-column selects): 1, or the interior + edge launches: 0.
-void set_xone(long v);
-long get_xone();
 void set_march_tile_rows(long v);
 long get_march_tile_rows();
 // Cross pass on row blocks of <= xtile_max_rows rows (default 4097): edges as

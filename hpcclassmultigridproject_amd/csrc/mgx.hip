@@ -1505,11 +1505,6 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgxi::g_dist_local_side = value;
         return MGX_OK;
     }
-    if (!strcmp(key, "xone")) {
-        if (value != 0 && value != 1) return fail(MGX_E_ARG, "xone must be 0 or 1");
-        mgx::set_xone(value);
-        return MGX_OK;
-    }
     if (!strcmp(key, "wpair")) {
         if (value != 0 && value != 1) return fail(MGX_E_ARG, "wpair must be 0 or 1");
         mgxi::g_wpair = value;
@@ -1632,10 +1627,6 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "wpair")) {
         *value = mgxi::g_wpair;
-        return MGX_OK;
-    }
-    if (!strcmp(key, "xone")) {
-        *value = mgx::get_xone();
         return MGX_OK;
     }
     if (!strcmp(key, "dist_min_rows")) {

@@ -93,27 +93,13 @@ struct XCfg {
 // exact (sepvel.h checks the range) -- from the lane's column factors, held
 // in registers for the whole march.
 //
-// F = true (with G = false: the whole level in ONE launch, no edge launch):
-// the unguarded march over every strip and every row, where the Dirichlet
-// boundary is kept by two cheap tests instead of the guarded kernel's
-// per-stage exec-mask branches: the row of a stage is wave-uniform, so a
-// stage on a row outside [1, n-1] is skipped by a scalar branch, and the two
-// boundary columns 0 and n are frozen by a lane-constant select on each
-// update (in0 / in1).  Lanes outside [0, n] (the halos of the two boundary
-// strips) and rows outside [0, n] (the first and last segments' warm-ups)
-// read clamped rows and columns and stay frozen or are never stored, and
-// only ever feed the frozen boundary, so every stored value is exact.  The
-// norm and restriction residuals take the guarded kernel's row / column tests
-// as selects.
-//
 // FM = true (fp_mode fma, stencil.h): each row's rhs enters the ring as f' =
 // f/d at its first use (A: the row's first stage, before the hand-off, so B
 // receives it scaled), the per-row coefficients are the m = -c/d of the
 // contracted update (one fma each), every update is four fmas and every
 // residual d*(update - u).  B's time-step rhs (RS) keeps the reference
 // expressions (gs.cpp:44, stored unscaled) and is scaled after.
-template <int WPB, int K, bool G, bool RS = false, bool SV = false, bool FM = false,
-          bool F = false>
+template <int WPB, int K, bool G, bool RS = false, bool SV = false, bool FM = false>
 __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     const double *__restrict__ uin, double *__restrict__ upost, double *__restrict__ upre,
     const double *__restrict__ rhs, const double *__restrict__ v1, const double *__restrict__ v2,
@@ -124,7 +110,6 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
     const double *__restrict__ sb1, const double *__restrict__ sa2,
     const double *__restrict__ sb2) {
     using X = XCfg<K>;
-    static_assert(!F || (!G && !RS), "the one-launch form is the unguarded march");
     constexpr int S = X::S, H = X::H, NR = X::NR, W = X::W, D = X::D, NU = X::NU,
                   NRD = X::NRD, EA = X::EA, EB = X::EB;
     // A's prefetch distances in steps: rhs/v rows XRV ahead of their first
@@ -277,26 +262,20 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             Coef cg = c;
             if (!GS) asm volatile("" : "+s"(cg.nu));
             // (the unguarded kernel only runs with d > 0: xsmooth_inst)
-            // (F: a wave-uniform row test, then the lane's column select)
-            const bool rowok = !F || (unsigned)(r - 1) < (unsigned)(n - 1);
             if (cs == 0) {
                 const double uW = dpp_shr1(ur[iR].y);
-                if (rowok && (!GS || (inr && in0))) {
-                    const double nv = FM ? fm_upd_t(d.r.x, d.x.x, d.y.x, ur[iN].x, uW, ur[iS].x,
-                                                    ur[iR].y, c)
-                                         : gs_point_t<!GS>(d.r.x, d.x.x, d.y.x, ur[iN].x, uW,
-                                                           ur[iS].x, ur[iR].y, cg);
-                    ur[iR].x = (!F || in0) ? nv : ur[iR].x;
-                }
+                if (!GS || (inr && in0))
+                    ur[iR].x = FM ? fm_upd_t(d.r.x, d.x.x, d.y.x, ur[iN].x, uW, ur[iS].x,
+                                             ur[iR].y, c)
+                                  : gs_point_t<!GS>(d.r.x, d.x.x, d.y.x, ur[iN].x, uW, ur[iS].x,
+                                                    ur[iR].y, cg);
             } else {
                 const double uE = dpp_shl1(ur[iR].x);
-                if (rowok && (!GS || (inr && in1))) {
-                    const double nv = FM ? fm_upd_t(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x,
-                                                    ur[iS].y, uE, c)
-                                         : gs_point_t<!GS>(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x,
-                                                           ur[iS].y, uE, cg);
-                    ur[iR].y = (!F || in1) ? nv : ur[iR].y;
-                }
+                if (!GS || (inr && in1))
+                    ur[iR].y = FM ? fm_upd_t(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x, ur[iS].y,
+                                             uE, c)
+                                  : gs_point_t<!GS>(d.r.y, d.x.y, d.y.y, ur[iN].y, ur[iR].x,
+                                                    ur[iS].y, uE, cg);
             }
         };
         // residual of the row in slot iR at column c0 / c0+1 from its t
@@ -360,30 +339,22 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
             const CoefRow &k = cf[iR];
             const double2 f = rd[iR].r;
             const bool inr = !GS || (r >= 1 && r <= n - 1);
-            // (F: a wave-uniform row test, then the lane's column select)
-            const bool rowok = !F || (unsigned)(r - 1) < (unsigned)(n - 1);
             if (cs == 0) {
                 const double uW = dpp_shr1(ur[iR].y);
-                if (rowok && (!GS || (inr && in0))) {
-                    const double nv =
-                        FM ? fm_upd(f.x, k.cn.x, ur[iN].x, k.cw.x, uW, k.cs.x, ur[iS].x, k.ce.x,
-                                    ur[iR].y)
-                           : div_diag<!GS>(f.x - k.cn.x * ur[iN].x - k.cw.x * uW -
-                                               k.cs.x * ur[iS].x - k.ce.x * ur[iR].y,
-                                           c);
-                    ur[iR].x = (!F || in0) ? nv : ur[iR].x;
-                }
+                if (!GS || (inr && in0))
+                    ur[iR].x = FM ? fm_upd(f.x, k.cn.x, ur[iN].x, k.cw.x, uW, k.cs.x, ur[iS].x,
+                                           k.ce.x, ur[iR].y)
+                                  : div_diag<!GS>(f.x - k.cn.x * ur[iN].x - k.cw.x * uW -
+                                                      k.cs.x * ur[iS].x - k.ce.x * ur[iR].y,
+                                                  c);
             } else {
                 const double uE = dpp_shl1(ur[iR].x);
-                if (rowok && (!GS || (inr && in1))) {
-                    const double nv =
-                        FM ? fm_upd(f.y, k.cn.y, ur[iN].y, k.cw.y, ur[iR].x, k.cs.y, ur[iS].y,
-                                    k.ce.y, uE)
-                           : div_diag<!GS>(f.y - k.cn.y * ur[iN].y - k.cw.y * ur[iR].x -
-                                               k.cs.y * ur[iS].y - k.ce.y * uE,
-                                           c);
-                    ur[iR].y = (!F || in1) ? nv : ur[iR].y;
-                }
+                if (!GS || (inr && in1))
+                    ur[iR].y = FM ? fm_upd(f.y, k.cn.y, ur[iN].y, k.cw.y, ur[iR].x, k.cs.y,
+                                           ur[iS].y, k.ce.y, uE)
+                                  : div_diag<!GS>(f.y - k.cn.y * ur[iN].y - k.cw.y * ur[iR].x -
+                                                      k.cs.y * ur[iS].y - k.ce.y * uE,
+                                                  c);
             }
         };
         // residual (gs.cpp:75 term order) at column c0 of the row in slot iR,
@@ -461,9 +432,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                             }
                         } else {   // acc + 0.0 == acc (acc >= +0): a select, no branch
                             const double r0 = res0();
-                            const bool ok = own(r) &&
-                                            (!F || ((unsigned)(r - 1) < (unsigned)(n - 1) && in0));
-                            acc += ok ? r0 * r0 : 0.0;
+                            acc += own(r) ? r0 * r0 : 0.0;
                         }
                     }
                     load_rv(s + XRV, (p + XRV) % NR);
@@ -504,9 +473,7 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                             }
                         } else {   // acc + 0.0 == acc (acc >= +0): a select, no branch
                             const double r1 = res_ty(iR, iN, iS, uE);
-                            const bool ok = own(r) &&
-                                            (!F || ((unsigned)(r - 1) < (unsigned)(n - 1) && in1));
-                            acc += ok ? r1 * r1 : 0.0;
+                            acc += own(r) ? r1 * r1 : 0.0;
                         }
                     }
                     if (RS) {
@@ -560,8 +527,8 @@ __global__ __launch_bounds__(128 * WPB) void k_xsmooth(
                         const int iN = (q - S + 2 * NR) % NR;
                         const int iS = (q + 2 - S + 2 * NR) % NR;
                         const double uW = dpp_shr1(ur[iR].y);
-                        const bool on = own(r) && (!(GN || F) || (r >= 1 && r <= n - 2 && in0 &&
-                                                                   c0 <= n - 2));
+                        const bool on = own(r) &&
+                                        (!GN || (r >= 1 && r <= n - 2 && in0 && c0 <= n - 2));
                         const double res = res_x(iR, iN, iS, uW);
                         st1_ifu(rhsc + rowoff(r >> 1, ipc), c0 >> 1, on, res);
                     }
@@ -837,16 +804,10 @@ __global__ __launch_bounds__(256) void k_xtile(
 }  // namespace
 
 long g_xfast = 1;   // unguarded interior march kernels (tuning key "xfast")
-// tuning key "xone": 1 = a whole level's cross pass as one launch of the
-// unguarded march with uniform row tests and boundary-column selects (F);
-// 0 = the interior launch + the guarded edge launch
-long g_xone = 0;
-void set_xone(long v) { g_xone = v; }
-long get_xone() { return g_xone; }
 void set_xfast(long v) { g_xfast = v; }
 long get_xfast() { return g_xfast; }
 
-template <int WPB, int K, bool G, bool RS, bool SV, bool FM, bool F = false>
+template <int WPB, int K, bool G, bool RS, bool SV, bool FM>
 static int xsmooth_slots() {
     static int slots = 0;   // resident workgroups of this instantiation
     if (!slots) {
@@ -854,7 +815,7 @@ static int xsmooth_slots() {
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per,
-                                                           k_xsmooth<WPB, K, G, RS, SV, FM, F>,
+                                                           k_xsmooth<WPB, K, G, RS, SV, FM>,
                                                            128 * WPB, 0);
         slots = std::max(1, cus) * std::max(1, per);
     }
@@ -864,7 +825,7 @@ static int xsmooth_slots() {
 // One launch over `reg`; min_rows: the fewest rows per workgroup (each
 // workgroup's march pays a warm-up of ~EA + EB + D rows).  Returns the norm
 // partials written (grid * 2 * WPB: one per wave) at `partials`.
-template <int WPB, int K, bool G, bool RS, bool SV, bool FM, bool F = false>
+template <int WPB, int K, bool G, bool RS, bool SV, bool FM>
 static int xsmooth_launch_sv(const XArgs &A, const MarchRegions &reg, double *partials, int lo,
                              int hi, long min_rows, long max_wgs, hipStream_t s) {
     const long total = reg.pre[reg.count];
@@ -872,12 +833,11 @@ static int xsmooth_launch_sv(const XArgs &A, const MarchRegions &reg, double *pa
     long upw;
     MarchRegions r;
     using X = XCfg<K>;
-    const unsigned grid = plan_march(reg, WPB, xsmooth_slots<WPB, K, G, RS, SV, FM, F>(),
-                                     min_rows, max_wgs, X::EA + X::EB + X::D + X::NR / 2, upw,
-                                     r);
+    const unsigned grid = plan_march(reg, WPB, xsmooth_slots<WPB, K, G, RS, SV, FM>(), min_rows,
+                                     max_wgs, X::EA + X::EB + X::D + X::NR / 2, upw, r);
     // RS: the second partials (the next step's initial norm) at the same
     // offsets, kNormBlocks further on
-    MGX_LAUNCH((k_xsmooth<WPB, K, G, RS, SV, FM, F>), dim3(grid), dim3(128 * WPB), s, A.uin,
+    MGX_LAUNCH((k_xsmooth<WPB, K, G, RS, SV, FM>), dim3(grid), dim3(128 * WPB), s, A.uin,
                A.upost, A.upre, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, partials, (int)A.n,
                A.pitch, r, upw, A.c, lo, hi, A.store_post ? 1 : 0, A.rhs_next,
                RS ? partials + kNormBlocks : (double *)nullptr, A.sa1, A.sb1, A.sa2, A.sb2);
@@ -885,22 +845,22 @@ static int xsmooth_launch_sv(const XArgs &A, const MarchRegions &reg, double *pa
 }
 // SV when the level's velocity factors are given (XArgs::sa1); FM = the
 // level's fp_mode (Coef::fm)
-template <int WPB, int K, bool G, bool RS = false, bool F = false>
+template <int WPB, int K, bool G, bool RS = false>
 static int xsmooth_launch(const XArgs &A, const MarchRegions &reg, double *partials, int lo, int hi,
                           long min_rows, long max_wgs, hipStream_t s) {
     const bool sv = A.sa1 && A.sb1 && A.sa2 && A.sb2;
     if (A.c.fm) {
         if (sv)
-            return xsmooth_launch_sv<WPB, K, G, RS, true, true, F>(A, reg, partials, lo, hi,
-                                                                  min_rows, max_wgs, s);
-        return xsmooth_launch_sv<WPB, K, G, RS, false, true, F>(A, reg, partials, lo, hi,
+            return xsmooth_launch_sv<WPB, K, G, RS, true, true>(A, reg, partials, lo, hi,
                                                                min_rows, max_wgs, s);
+        return xsmooth_launch_sv<WPB, K, G, RS, false, true>(A, reg, partials, lo, hi, min_rows,
+                                                            max_wgs, s);
     }
     if (sv)
-        return xsmooth_launch_sv<WPB, K, G, RS, true, false, F>(A, reg, partials, lo, hi, min_rows,
-                                                               max_wgs, s);
-    return xsmooth_launch_sv<WPB, K, G, RS, false, false, F>(A, reg, partials, lo, hi, min_rows,
+        return xsmooth_launch_sv<WPB, K, G, RS, true, false>(A, reg, partials, lo, hi, min_rows,
                                                             max_wgs, s);
+    return xsmooth_launch_sv<WPB, K, G, RS, false, false>(A, reg, partials, lo, hi, min_rows,
+                                                         max_wgs, s);
 }
 
 static void add_tile_region(TileRegions &r, int c0, int c1, int r0, int r1, int TR) {
@@ -1021,15 +981,6 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
     // the unguarded kernel's division assumes d > 0 (div_diag<true>)
     const bool split = g_xfast != 0 && A.c.dgs > 0;
     if (A.phase != 0 && !split) return -1;   // a split pass needs the split kernels
-    if (split && g_xone && A.phase == 0 && A.rb < 0) {
-        // the whole level as ONE launch of the unguarded march (F: uniform
-        // row tests, boundary columns frozen by a select), no edge launch
-        const int strips = (int)((n + 1 + X::W - 1) / X::W);
-        MarchRegions all{};
-        add_region<WPB>(all, 0, strips, ra, rb);
-        return xsmooth_launch<WPB, K, false, false, true>(A, all, A.partials, lo, hi, A.min_rows,
-                                                          kNormBlocks / (2 * WPB) / 2, s);
-    }
     if (split && rb - ra <= g_xtile_max_rows) {
         const int r = xsmooth_tiled<WPB, K>(A, ra, rb, lo, hi, s);
         if (r != -2) return r;

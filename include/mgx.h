@@ -209,10 +209,6 @@ int mgx_synchronize(mgx_ctx *ctx);
  * "xfast": 1 (default) runs the cross-cycle pass as an unguarded kernel over
  * the interior strips and rows plus a guarded kernel over the boundary strips
  * and bands; 0 = one guarded launch (bitwise the same results).
- * "xone": 1 runs a whole level's cross-cycle pass as ONE launch of the
- * unguarded kernel (the boundary rows skipped by wave-uniform row tests, the
- * boundary columns frozen by lane selects) instead of the interior + edge
- * launches; 0 = the two launches.  Bitwise the same results.
  * "march_tile_rows": a row block whose wave march would give each resident
  * workgroup fewer than this many rows runs as LDS tiles (default 16, >= 0).
  * "xtile_max_rows": on row blocks of at most this many rows (a rank of a

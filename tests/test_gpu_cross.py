@@ -259,28 +259,6 @@ def test_wcycle_cross_passes_equal_unfused(N, L, kw, cross):
     np.testing.assert_allclose(n_x, n_ref, rtol=NORM_RTOL)
 
 
-@pytest.mark.parametrize("N,L,kw", [
-    (16384, 9, {}), (16384, 9, dict(fp_mode=_lib.FP_FMA)),
-    (4096, 7, dict(nsmooth=2)), (4096, 6, dict(fp_mode=_lib.FP_FMA, tower_mode=_lib.TOWER_CORRECT)),
-    (8192, 5, dict(shape=2))], ids=["N16384", "N16384fma", "N4096nu2", "N4096fma_correct", "W8192"])
-def test_cross_pass_one_launch_equals_split(N, L, kw, knobs):
-    """xone: the whole level's cross pass as ONE launch of the unguarded march
-    (uniform row tests, boundary columns frozen by selects) -- bitwise the
-    interior + guarded edge launches, norms to the summation-order tolerance."""
-    out = {}
-    for x in (0, 1):
-        knobs(xone=x)
-        u0, v1, v2 = init_problem(N)
-        with Multigrid(N, L, 1.0 / N / 10, NU, **kw) as mg:
-            mg.upload(u0, v1, v2)
-            mg.rhs()
-            norms = [mg.run_cycles(1) for _ in range(3)] + [mg.run_cycles(2)]
-            out[x] = (mg.download(), norms, mg.mg_outer(1e-9)[:2])
-    assert np.array_equal(out[1][0], out[0][0])
-    np.testing.assert_allclose(out[1][1], out[0][1], rtol=NORM_RTOL)
-    assert out[1][2][0] == out[0][2][0]
-
-
 @pytest.mark.parametrize("nsmooth", [1, 2, 3])
 @pytest.mark.parametrize("fp", [_lib.FP_BITWISE, _lib.FP_FMA], ids=["bitwise", "fma"])
 def test_wcycle_tile_pairs_equal_unfused_and_oracle(oracle_mod, knobs, nsmooth, fp):
