@@ -89,6 +89,10 @@ struct mgx_ctx {
     // mg_outer's cycle predicted to be the last: its finest level runs the
     // post-smoothing alone, not the cross pass (no next-cycle pre-smoothing)
     bool post_only = false;
+    // the coarsest solve of level cf_level (cf_reps solves) deferred into the
+    // prolongation tile pass of the level above (tuning key "coarse_fuse");
+    // -1: none pending
+    int cf_level = -1, cf_reps = 0;
     // time-step mode: inside mgx_step (step_next) the last cycle's cross pass
     // also forms the next step's rhs (lv[0].rhs_alt), initial norm
     // (step_res0) and first pre-smoothing + restriction (lv[0].spec, lv[1]

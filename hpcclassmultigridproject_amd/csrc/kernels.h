@@ -96,6 +96,26 @@ void launch_vgen_check(const double *v1, const double *v2, long n, long pitch, V
 // of rows another rank factored, read from this rank's exchanged ghost rows
 void launch_vgen_fill_rows(double2 *a, const double *v1, const double *v2, long pitch, int l,
                            int js1, int js2, int r0, int r1, hipStream_t s);
+// the coarsest solve with u in LDS (stencil.h coarse_lds_body): levels n <= 64
+constexpr int kCoarseLdsMaxN = 64;
+constexpr int kCoarseLdsNP = kCoarseLdsMaxN + 1;
+
+// The coarsest level's solve fused into the tile pass above it (k_smooth_tile
+// with prolongation): every workgroup solves the coarsest level in LDS
+// (stencil.h coarse_lds_body, n <= kCoarseLdsMaxN) and prolongs from that
+// copy; the workgroup of blockIdx 0 also stores u and the iteration counts.
+// on = 0: the pass reads the coarse u from HBM (uc).
+struct CoarseFuse {
+    double *u = nullptr;
+    const double *rhs = nullptr, *v1 = nullptr, *v2 = nullptr;
+    long n = 0, pitch = 0;
+    Coef c{};
+    double tol = 0.0;
+    int maxit = 0, zero_first = 0, reps = 0;
+    double *stats = nullptr;
+    int on = 0;
+};
+
 struct SmoothArgs {
     const double *uin;
     double *uout;
@@ -123,6 +143,10 @@ struct SmoothArgs {
     // field pointers are offset so that ptr + r*pitch is global row r.
     // rb < 0 means the whole level: ra = 0, rb = n+1, lo = 0, hi = n.
     int ra = 0, rb = -1, lo = 0, hi = -1;
+    // prolongation passes on tiles only: the coarse level solved in the pass
+    // (launch_smooth / launch_smooth_wpair return -4 when the pass would
+    // march instead)
+    CoarseFuse cf{};
 };
 int launch_smooth(const SmoothArgs &a, int sweeps, int mode, hipStream_t s);
 // A W-cycle's post-smoothing of one visit + pre-smoothing of the next on a tile

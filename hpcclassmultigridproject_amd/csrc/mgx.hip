@@ -152,6 +152,53 @@ static mgx::VGen level_vgen(const mgx_ctx *c, int l) {
     g.strided = c->opt.tower_mode == MGX_TOWER_CORRECT ? 1 : 0;
     return g;
 }
+// tuning key "coarse_fuse": 1 (default) = the coarsest solve (n <= 64, u in
+// LDS) runs inside the prolongation tile pass of the level above: every
+// workgroup of that pass solves the coarsest level in its LDS and prolongs
+// from the copy (mgx::CoarseFuse), one launch less per visit -- bitwise the
+// same; 0 = its own launch (op_coarse)
+long g_coarse_fuse = 1;
+int op_coarse(mgx_ctx *c, int l, int reps);
+// (only from a zero start, the V- and W-cycle's case after the restriction:
+// then no workgroup reads the coarse u that workgroup 0 stores at its end)
+static bool coarse_fusable(const mgx_ctx *c, int l) {
+    return g_coarse_fuse && !c->dist && c->opt.smoother == 0 && l == c->L - 1 && l >= 2 &&
+           c->lv[l].zero &&
+           c->lv[l].n <= mgx::kCoarseLdsMaxN && mgx::get_coarse_lds() &&
+           c->lv[l - 1].n <= mgx::get_tile_max_n();
+}
+// run a pending fused coarsest solve on its own (its consumer cannot take it)
+static int flush_coarse(mgx_ctx *c) {
+    if (c->cf_level < 0) return MGX_OK;
+    const int l = c->cf_level;
+    c->cf_level = -1;
+    return op_coarse(c, l, c->cf_reps);
+}
+// the pending coarsest solve of level l+1 into a prolongation pass of level l
+static bool take_coarse(mgx_ctx *c, int l, mgx::SmoothArgs &A) {
+    if (c->cf_level != l + 1) return false;
+    Level &Cl = c->lv[l + 1];
+    A.cf.u = Cl.U();
+    A.cf.rhs = Cl.rhs;
+    A.cf.v1 = Cl.v1;
+    A.cf.v2 = Cl.v2;
+    A.cf.n = Cl.n;
+    A.cf.pitch = Cl.pitch;
+    A.cf.c = Cl.coef;
+    A.cf.tol = c->opt.coarse_tol;
+    A.cf.maxit = c->opt.coarse_maxit;
+    A.cf.zero_first = Cl.zero ? 1 : 0;
+    A.cf.reps = c->cf_reps;
+    A.cf.stats = c->dscal + 2;
+    A.cf.on = 1;
+    return true;
+}
+// after a launch that took it: the coarse level holds its solution
+static void took_coarse(mgx_ctx *c, int l) {
+    c->cf_level = -1;
+    c->lv[l + 1].zero = false;
+}
+
 int op_smooth(mgx_ctx *c, int l, int sweeps, bool prolong, bool restrict_, bool norm,
               bool *fused_norm) {
     Level &L = c->lv[l];
@@ -165,7 +212,10 @@ int op_smooth(mgx_ctx *c, int l, int sweeps, bool prolong, bool restrict_, bool 
             const bool pr = prolong && first && !L.zero;
             const bool rs = restrict_ && last;
             const bool nm = norm && last && !rs;
-            if (pr) CHK(materialize(c, l + 1));
+            // a pending coarsest solve of level l+1 runs inside this pass
+            // (its u is then not read from HBM: no zero fill either)
+            const bool cfuse = pr && c->cf_level == l + 1;
+            if (pr && !cfuse) CHK(materialize(c, l + 1));
             int mode = 0;
             if (L.zero) mode |= mgx::kModeZero;
             if (pr) mode |= mgx::kModeProlong;
@@ -191,6 +241,7 @@ int op_smooth(mgx_ctx *c, int l, int sweeps, bool prolong, bool restrict_, bool 
             }
             A.partials = c->partials;
             A.norm_out = c->dscal;
+            if (cfuse) take_coarse(c, l, A);
             double bytes = 40.0 * k * L.M();
             int kind = MGX_K_GS;
             if (pr) {
@@ -210,6 +261,17 @@ int op_smooth(mgx_ctx *c, int l, int sweeps, bool prolong, bool restrict_, bool 
             int blocks = 0;
             CHK(launch(c, kind, l, bytes, cbytes,
                        [&] { blocks = mgx::launch_smooth(A, k, mode, c->stream); }));
+            if (blocks == -4 && cfuse) {
+                // the pass would march: the coarsest solve on its own, then the pass
+                // (nothing was launched)
+                A.cf = mgx::CoarseFuse{};
+                CHK(flush_coarse(c));
+                A.uc = c->lv[l + 1].U();
+                CHK(launch(c, kind, l, bytes, cbytes,
+                           [&] { blocks = mgx::launch_smooth(A, k, mode, c->stream); }));
+            } else if (cfuse) {
+                took_coarse(c, l);
+            }
             if (blocks < 0) return fail(MGX_E_ARG, "launch_smooth: unsupported sweeps/mode");
             L.cur = L.nxt();
             L.zero = false;
@@ -299,8 +361,9 @@ int op_wpair(mgx_ctx *c, int l, bool *done) {
     *done = false;
     Level &L = c->lv[l], &Cl = c->lv[l + 1];
     const int k = c->opt.nsmooth;
+    const bool cfuse = c->cf_level == l + 1;   // the coarsest solve pending, fused
     if (!g_wpair || c->opt.smoother != 0 || k < 1 || k > 3 || c->opt.fuse < k || L.zero ||
-        Cl.zero)
+        (Cl.zero && !cfuse))
         return MGX_OK;
     mgx::SmoothArgs A{};
     A.uin = L.u[L.cur];
@@ -316,6 +379,7 @@ int op_wpair(mgx_ctx *c, int l, bool *done) {
     A.pitchc = Cl.pitch;
     A.partials = c->partials;
     A.norm_out = c->dscal;
+    if (cfuse) take_coarse(c, l, A);
     // post (prolong + add, k sweeps) + pre (k sweeps, restrict)
     const double bytes = (32.0 + 40.0 * k) * L.M() + 8.0 * Cl.M() + (40.0 * k + 40.0) * L.M() +
                          24.0 * Cl.M();
@@ -323,7 +387,9 @@ int op_wpair(mgx_ctx *c, int l, bool *done) {
     int blocks = 0;
     CHK(launch(c, MGX_K_PSMOOTH, l, bytes, cbytes,
                [&] { blocks = mgx::launch_smooth_wpair(A, k, c->stream); }));
+    if (blocks == -4) return flush_coarse(c);   // nothing launched: the two passes
     if (blocks < 0) return MGX_OK;   // a march level: the two passes as usual
+    if (cfuse) took_coarse(c, l);
     L.cur = L.nxt();
     Cl.zero = true;
     *done = true;
@@ -497,7 +563,12 @@ int op_vcycle(mgx_ctx *c, int l, double *norm, bool store_post) {
     for (int sh = 0; sh < (l == c->L - 1 ? 1 : c->opt.shape); ++sh) {
         const bool last = sh == c->opt.shape - 1;
         if (l == c->L - 1) {
-            CHK(op_coarse(c, l, c->opt.shape));
+            if (coarse_fusable(c, l)) {   // taken by the next prolongation pass
+                c->cf_level = l;
+                c->cf_reps = c->opt.shape;
+            } else {
+                CHK(op_coarse(c, l, c->opt.shape));
+            }
         } else {
             if (!pre_done)
                 CHK(op_smooth(c, l, c->opt.nsmooth, false, /*restrict=*/true, false, nullptr));
@@ -515,6 +586,7 @@ int op_vcycle(mgx_ctx *c, int l, double *norm, bool store_post) {
             }
             CHK(op_smooth(c, l, c->opt.nsmooth, /*prolong=*/true, false, norm && last,
                           &have_norm));
+            CHK(flush_coarse(c));   // (taken above; never left pending)
         }
     }
     if (norm) {
@@ -1505,6 +1577,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgxi::g_dist_local_side = value;
         return MGX_OK;
     }
+    if (!strcmp(key, "coarse_fuse")) {
+        if (value != 0 && value != 1) return fail(MGX_E_ARG, "coarse_fuse must be 0 or 1");
+        mgxi::g_coarse_fuse = value;
+        return MGX_OK;
+    }
     if (!strcmp(key, "wpair")) {
         if (value != 0 && value != 1) return fail(MGX_E_ARG, "wpair must be 0 or 1");
         mgxi::g_wpair = value;
@@ -1623,6 +1700,10 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "dist_comm_chain")) {
         *value = mgxi::g_dist_comm_chain;
+        return MGX_OK;
+    }
+    if (!strcmp(key, "coarse_fuse")) {
+        *value = mgxi::g_coarse_fuse;
         return MGX_OK;
     }
     if (!strcmp(key, "wpair")) {

@@ -530,4 +530,163 @@ MarchRegions order_regions(const MarchRegions &reg, long upw);
 unsigned plan_march(const MarchRegions &reg, int wpb, long slots, long min_rows, long max_wgs,
                     int warm, long &upw, MarchRegions &out);
 
+
+// ------------------------------------------------------- coarsest solve in LDS
+// The coarsest solve (k_coarse_solve, kernels.hip) with u held in LDS and each thread's rhs / v1 / v2 (FM: f',
+// t1, t2) in registers (n <= 64): the loop touches no global memory.  Same
+// sweep order, term order and reduction order as k_coarse_solve, so u, the
+// norms and the iteration count are bitwise those of k_coarse_solve.
+//
+// Latency and LDS issue, not work, are the cost of this kernel (~4 K points):
+//   * the colour stages map the 1024 threads onto the colour's points as
+//     (row 1 + (t >> 5) + 32p, the colour's column 2(t & 31) + 1 or + 2): two
+//     points per thread, every lane busy (k_coarse_solve's layout leaves half
+//     the lanes idle and gives the others four rows each), and each stage
+//     first reads the neighbours of both points, then stores both updates
+//     (the points of a colour are independent);
+//   * the residual keeps k_coarse_solve's layout (rows 1 + ty + 16m, column
+//     1 + tx) and its summation order (rows m ascending, then the wave
+//     butterfly, then the 16 waves in order), so the norms are its bits;
+//   * every loop is unrolled to its fixed trip count for n <= 64, guarded.
+// reps: the solve repeated back to back (a W-cycle visits the coarsest level
+// `shape` times in a row, multigrid.cpp:52-65) in this one launch.
+//
+// As a device function for one workgroup of 1024 threads: k_coarse_solve_lds
+// (kernels.hip) is this alone; k_smooth_tile (wsmooth.hip, CoarseFuse) runs it
+// first in every workgroup of the pass above the coarsest level and prolongs
+// from the LDS copy (write = false in all but one workgroup, which stores u
+// and the iteration statistics as the kernel does).  su: kCoarseLdsNP^2
+// doubles of LDS, lds: 16, s_norm: 1.
+// (kCoarseLdsMaxN, kCoarseLdsNP: kernels.h)
+template <bool FM>
+__device__ __forceinline__ void coarse_lds_body(double *su, double *lds, double *s_norm, double *u,
+                                                const double *rhs, const double *v1,
+                                                const double *v2, int n, long pitch, Coef c,
+                                                double tol, int maxit, int zero_first, int reps,
+                                                double *stats, bool write) {
+    constexpr int NP = kCoarseLdsNP;
+    constexpr int MR = kCoarseLdsMaxN / 16;   // residual rows per thread: 1 + ty + 16m <= 64
+    constexpr int GP = kCoarseLdsMaxN / 32;   // colour points per thread: rows 1 + r + 32p
+    const int t = threadIdx.x;
+    const int tx = t & 63, ty = t >> 6;
+    const int gk = t & 31, gr = t >> 5;
+    const double hh = c.h * 0.5;
+    // per-point constants in registers: (f, t1, t2) = FM ? (rhs/d, v1*h/2, v2*h/2)
+    // : (rhs, v1, v2), exactly the operands the L2 version reads per use
+    auto consts = [&](long p, double &f, double &x, double &y) {
+        const double r = rhs[p], a = v1[p], b = v2[p];
+        f = FM ? r * c.rdgs : r;
+        x = FM ? a * hh : a;
+        y = FM ? b * hh : b;
+    };
+    double gf[2][GP], gx[2][GP], gy[2][GP];   // colour points
+    int gq[2][GP];
+    bool gon[2][GP];
+    double rf[MR], rx[MR], ry[MR];            // residual points
+    int rq[MR];
+    bool ron[MR];
+#pragma unroll
+    for (int colour = 0; colour < 2; ++colour)
+#pragma unroll
+        for (int p = 0; p < GP; ++p) {
+            const int i = 1 + gr + 32 * p;
+            const int j = 1 + ((i + 1 + colour) & 1) + 2 * gk;
+            gon[colour][p] = i <= n - 1 && j <= n - 1;
+            gq[colour][p] = gon[colour][p] ? i * NP + j : NP + 1;
+            gf[colour][p] = gx[colour][p] = gy[colour][p] = 0.0;
+            if (gon[colour][p])
+                consts((long)i * pitch + j, gf[colour][p], gx[colour][p], gy[colour][p]);
+        }
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+        const int i = 1 + ty + 16 * m, j = 1 + tx;
+        ron[m] = i <= n - 1 && j <= n - 1;
+        rq[m] = ron[m] ? i * NP + j : NP + 1;
+        rf[m] = rx[m] = ry[m] = 0.0;
+        if (ron[m]) consts((long)i * pitch + j, rf[m], rx[m], ry[m]);
+    }
+    {   // u into LDS: rows ty + 16m (m <= 4), columns tx, tx + 64, all loads in flight
+        constexpr int MF = (kCoarseLdsMaxN + 16) / 16;
+        double a[MF][2];
+#pragma unroll
+        for (int m = 0; m < MF; ++m)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int i = ty + 16 * m, j = tx + 64 * h;
+                a[m][h] = 0.0;
+                if (!zero_first && i <= n && j <= n) a[m][h] = u[(long)i * pitch + j];
+            }
+#pragma unroll
+        for (int m = 0; m < MF; ++m)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int i = ty + 16 * m, j = tx + 64 * h;
+                if (i <= n && j <= n) su[i * NP + j] = a[m][h];
+            }
+    }
+    if (write && zero_first)   // (the row padding, as the L2 version leaves it)
+        for (int i = ty; i <= n; i += 16)
+            for (int j = n + 1 + tx; j < pitch; j += 64) u[(long)i * pitch + j] = 0.0;
+    __syncthreads();
+    int total = 0;
+    double res = 1.0;
+    for (int rep = 0; rep < reps; ++rep) {
+        int it = 0;
+        res = 1.0;
+        while (it < maxit && res > tol) {
+#pragma unroll
+            for (int colour = 0; colour < 2; ++colour) {
+                double nN[GP], nW[GP], nS[GP], nE[GP];
+#pragma unroll
+                for (int p = 0; p < GP; ++p) {
+                    const int q = gq[colour][p];
+                    nN[p] = su[q - NP];
+                    nW[p] = su[q - 1];
+                    nS[p] = su[q + NP];
+                    nE[p] = su[q + 1];
+                }
+#pragma unroll
+                for (int p = 0; p < GP; ++p) {
+                    if (!gon[colour][p]) continue;
+                    su[gq[colour][p]] =
+                        FM ? fm_upd_t(gf[colour][p], gx[colour][p], gy[colour][p], nN[p], nW[p],
+                                      nS[p], nE[p], c)
+                           : gs_point(gf[colour][p], gx[colour][p], gy[colour][p], nN[p], nW[p],
+                                      nS[p], nE[p], c);
+                }
+                __syncthreads();
+            }
+            double acc = 0.0;
+            {
+                double rr[MR];
+#pragma unroll
+                for (int m = 0; m < MR; ++m) {
+                    const int q = rq[m];
+                    rr[m] = FM ? fm_res_t(rf[m], rx[m], ry[m], su[q], su[q - NP], su[q - 1],
+                                          su[q + NP], su[q + 1], c)
+                               : res_point(rf[m], rx[m], ry[m], su[q], su[q - NP], su[q - 1],
+                                           su[q + NP], su[q + 1], c);
+                }
+#pragma unroll
+                for (int m = 0; m < MR; ++m)
+                    if (ron[m]) acc += rr[m] * rr[m];
+            }
+            double s = block_sum(acc, lds);
+            if (t == 0) *s_norm = sqrt(s);
+            __syncthreads();
+            res = *s_norm;
+            ++it;
+            __syncthreads();
+        }
+        total += it;
+    }
+    if (!write) return;
+    for (int i = ty; i <= n; i += 16)
+        for (int j = tx; j <= n; j += 64) u[(long)i * pitch + j] = su[i * NP + j];
+    if (t == 0) {
+        stats[0] += total;
+        stats[1] = res;
+    }
+}
+
 }  // namespace mgx

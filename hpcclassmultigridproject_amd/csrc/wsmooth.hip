@@ -527,7 +527,7 @@ __global__ __launch_bounds__(MGX_TILE_THREADS) void k_smooth_tile(
     const double *__restrict__ uin, double *__restrict__ uout, const double *__restrict__ rhs,
     const double *__restrict__ v1, const double *__restrict__ v2, const double *__restrict__ uc,
     long pitchc, double *__restrict__ rhsc, double *__restrict__ partials, int n, long pitch,
-    int tiles_x, Coef c, int ra, int rb, int lo, int hi, int xcd) {
+    int tiles_x, Coef c, int ra, int rb, int lo, int hi, int xcd, CoarseFuse cf) {
     using C = SmoothCfg<K, MODE>;
     using T = TileCfg<K, MODE, TRV>;
     constexpr int S = C::S, EH = T::EH, WT = T::WT, PPT = T::PPT, HW = WT / 2;
@@ -549,6 +549,23 @@ __global__ __launch_bounds__(MGX_TILE_THREADS) void k_smooth_tile(
     const long i0 = ra + (long)ty * T::TR - EH, j0 = (long)tx * T::TC - EH;   // tile origin (even)
     const int nc = n >> 1;
 
+    // cf.on (prolongation passes): the coarse level is solved here first, in
+    // LDS, by every workgroup alike (the same operations: the same bits), and
+    // the prolongation reads that copy; workgroup 0 stores it (CoarseFuse)
+    __shared__ double csu[C::PROL ? kCoarseLdsNP * kCoarseLdsNP : 1];
+    __shared__ double cred[C::PROL ? 16 : 1];
+    __shared__ double cnorm;
+    if constexpr (C::PROL) {
+        if (cf.on)
+            coarse_lds_body<FM>(csu, cred, &cnorm, cf.u, cf.rhs, cf.v1, cf.v2, (int)cf.n,
+                                cf.pitch, cf.c, cf.tol, cf.maxit, cf.zero_first, cf.reps,
+                                cf.stats, blockIdx.x == 0);
+    }
+    // coarse u (i, j): the LDS copy or HBM
+    auto cu = [&](long i, long j) {
+        return (C::PROL && cf.on) ? csu[i * kCoarseLdsNP + j] : uc[i * pitchc + j];
+    };
+
     // rhs / v1 / v2 of the lane's pairs as scalar arrays (static indices only,
     // so they stay in registers)
     double f0[PPT], f1[PPT], x0[PPT], x1[PPT], y0[PPT], y1[PPT];
@@ -568,14 +585,14 @@ __global__ __launch_bounds__(MGX_TILE_THREADS) void k_smooth_tile(
             if (!C::ZERO) v = ld2(uin + o);
             if (C::PROL) {
                 const long ii = gi >> 1, jj = gj >> 1;
-                const double *p0 = uc + ii * pitchc + jj;
-                const double q00 = p0[0], q01 = (jj + 1 <= nc) ? p0[1] : 0.0;
+                const double q00 = cu(ii, jj), q01 = (jj + 1 <= nc) ? cu(ii, jj + 1) : 0.0;
                 double2 pr;
                 if (!(gi & 1)) {
                     pr.x = q00;
                     pr.y = (q00 + q01) / 2;
                 } else {
-                    const double q10 = p0[pitchc], q11 = (jj + 1 <= nc) ? p0[pitchc + 1] : 0.0;
+                    const double q10 = cu(ii + 1, jj),
+                                 q11 = (jj + 1 <= nc) ? cu(ii + 1, jj + 1) : 0.0;
                     pr.x = (q00 + q10) / 2;
                     pr.y = (q00 + q10 + q01 + q11) / 4;
                 }
@@ -770,11 +787,11 @@ static int smooth_tile_rows(const SmoothArgs &A, hipStream_t s) {
     if (A.c.fm)
         MGX_LAUNCH((k_smooth_tile<K, MODE, TRV, true>), dim3((unsigned)grid), dim3(T::THREADS), s,
                    A.uin, A.uout, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, A.partials, (int)n,
-                   A.pitch, tiles_x, A.c, A.ra, A.rb, A.lo, A.hi, g_tile_xcd ? 1 : 0);
+                   A.pitch, tiles_x, A.c, A.ra, A.rb, A.lo, A.hi, g_tile_xcd ? 1 : 0, A.cf);
     else
         MGX_LAUNCH((k_smooth_tile<K, MODE, TRV, false>), dim3((unsigned)grid), dim3(T::THREADS), s,
                    A.uin, A.uout, A.rhs, A.v1, A.v2, A.uc, A.pitchc, A.rhsc, A.partials, (int)n,
-                   A.pitch, tiles_x, A.c, A.ra, A.rb, A.lo, A.hi, g_tile_xcd ? 1 : 0);
+                   A.pitch, tiles_x, A.c, A.ra, A.rb, A.lo, A.hi, g_tile_xcd ? 1 : 0, A.cf);
     return (int)grid;
 }
 
@@ -822,10 +839,14 @@ static bool smooth_as_tiles(const SmoothArgs &A) {
 template <int K, int MODE>
 static int smooth_block(const SmoothArgs &A, hipStream_t s) {
     const bool tile = smooth_as_tiles<K, MODE>(A);
+    // a fused coarse solve needs the tile pass (the march reads uc from HBM)
+    const bool fused = A.cf.on && (MODE & kModeProlong) && A.cf.n <= kCoarseLdsMaxN;
+    if (A.cf.on && !fused) return -4;
     if (tile) {
         const int g = smooth_tile_inst<K, MODE>(A, s);
         if (g > 0) return g;
     }
+    if (fused) return -4;
     // the wave-private row march (also the fallback when a tile launch would
     // need more norm partials than the buffer holds)
     return smooth_winst<4, K, MODE>(A, s);
@@ -877,6 +898,7 @@ int launch_smooth_wpair(const SmoothArgs &A0, int nsmooth, hipStream_t s) {
         A.hi = (int)A.n;
     }
     if (A.ra & 1) return -1;
+    if (A.cf.on && A.cf.n > kCoarseLdsMaxN) return -4;
     constexpr int M = kModeProlong | kModeRestrict;
     switch (nsmooth) {
         case 1:

@@ -247,6 +247,13 @@ int mgx_synchronize(mgx_ctx *ctx);
  * forms the next step's rhs, initial norm and first pre-smoothing, which the
  * next mgx_step starts from (any other call in between drops them); 0 = each
  * step starts with its own rhs + norm pass.
+ * "coarse_fuse": 1 (default) runs the coarsest solve (n <= 64, with
+ * coarse_lds) inside the prolongation tile pass of the level above: every
+ * workgroup of that pass solves the coarsest level in its LDS and prolongs
+ * from the copy, one stores it -- no coarse launch, bitwise the same results,
+ * norms and iteration counts; 0 = its own launch.  Single-GPU contexts and
+ * the replicated levels of a partitioned one, when the level above runs as
+ * LDS tiles and the coarsest is level 2 or deeper.
  * "coarse_lds": 1 (default) solves coarsest levels n <= 64 with u in LDS
  * and each thread's rhs / v1 / v2 in registers, 0 = through L2 (bitwise the
  * same).  A W-cycle's `shape` consecutive solves of the coarsest level run in

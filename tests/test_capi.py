@@ -87,7 +87,7 @@ def test_init_problem_rows_are_rows_of_the_full_init():
 
 TUNING_KEYS = {   # key -> (a valid value, an invalid value or None)
     "tile_max_n": (1024, None), "cross_cycle": (0, 2),
-    "dist_min_rows": (64, 7), "xfast": (0, 2), "dist_overlap": (-1, 3), "dist_local_side": (1, 2), "dist_comm_chain": (0, 2), "wpair": (0, 2),
+    "dist_min_rows": (64, 7), "xfast": (0, 2), "dist_overlap": (-1, 3), "dist_local_side": (1, 2), "dist_comm_chain": (0, 2), "wpair": (0, 2), "coarse_fuse": (0, 2),
     "tile32_min_n": (1024, -1), "tile_xcd": (0, 2), "march_order": (1, 4),
     "march_min_rows": (96, 4), "coarse_lds": (0, 2), "step_fuse": (0, 2), "march_seg": (0, 2), "xtile_max_rows": (0, -1),
     "post_predict": (-1, -2), "post_only": (-1, -2), "step_cross": (0, 2),

@@ -201,6 +201,39 @@ def test_coarse_solve_in_lds_equals_l2_version(N, L, shape, knobs):
     assert np.array_equal(ua, ub) and ca == cb and ia == ib and ra == rb
 
 
+@pytest.mark.parametrize("N,L,shape,fp,parts", [
+    (2048, 6, 1, _lib.FP_BITWISE, 0), (2048, 6, 2, _lib.FP_FMA, 0), (4096, 7, 2, _lib.FP_BITWISE, 0),
+    (256, 3, 1, _lib.FP_FMA, 0), (1024, 5, 2, _lib.FP_FMA, 2)],
+    ids=["V2048", "W2048fma", "W4096", "V256fma", "W1024fma_parts2"])
+def test_coarse_fuse_equals_separate_launch(N, L, shape, fp, parts, knobs):
+    """coarse_fuse: the coarsest solve (n = 64, u in LDS) inside the tile pass
+    that prolongs from it -- every workgroup solves it in its LDS, workgroup 0
+    stores it -- is bitwise the separate k_coarse_solve_lds launch: the
+    solution, the norms, the coarse iteration counts and the coarsest level's
+    stored u; no coarse launch remains."""
+    out = []
+    u0, v1, v2 = init_problem(N)
+    for v in (0, 1):
+        knobs(coarse_fuse=v)
+        with Multigrid(N, L, 1.0 / N / 10, NU, shape=shape, fp_mode=fp,
+                       local_parts=parts) as mg:
+            mg.upload(u0, v1, v2)
+            mg.rhs()
+            mg.profile(True)
+            norms = [mg.run_cycles(1) for _ in range(3)]
+            cl = mg.profile_get(_lib.K_COARSE)[0]
+            mg.profile(False)
+            cyc = mg.step(1e-6)
+            coarsest = None if parts else mg.download_level(L - 1)
+            out.append((mg.download(), norms, cyc, mg.coarse_iterations(), coarsest, cl))
+    (ua, na, ca, ia, za, la), (ub, nb, cb, ib, zb, lb) = out
+    assert np.array_equal(ua, ub)
+    assert na == nb and ca == cb and ia == ib
+    if za is not None:
+        assert np.array_equal(za, zb)
+    assert la > 0 and lb == 0
+
+
 def test_negative_diagonal_routes_to_general_division(cross, oracle_mod):
     """nu > 0 large enough that the finest level's diagonal 1-4*rr*nu is
     negative: the unguarded cross kernel's division form assumes d > 0, so the
@@ -285,7 +318,9 @@ def test_wcycle_tile_pairs_equal_unfused_and_oracle(oracle_mod, knobs, nsmooth, 
     assert np.array_equal(out[1][0], out[0][0])
     assert out[1][3] == out[0][3]                  # the same coarse iterations
     assert out[1][1] < out[0][1], (out[0][1], out[1][1])
-    assert out[0][2] == out[1][2] == 2 * 2 ** (L - 1)   # one launch per coarsest visit
+    # one launch per coarsest visit, or none with the solve fused into the
+    # level above's prolongation pass (coarse_fuse, the default)
+    assert out[0][2] == out[1][2] == (0 if _lib.get_tuning("coarse_fuse") else 2 * 2 ** (L - 1))
     if fp == _lib.FP_BITWISE:
         O = oracle_mod
         O.set_threads(8)
