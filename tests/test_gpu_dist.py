@@ -181,8 +181,7 @@ def test_partitioned_refuses_per_level_ops_and_profiles(min_rows):
         coarse = mg.profile_get(_lib.K_COARSE)
         smooth = mg.profile_get(_lib.K_GS, 0)
         mg.profile(False)
-    # 2 cycles x 2 replicas (none with the coarsest solve fused, coarse_fuse)
-    assert halo[0] > 0 and coarse[0] == (0 if _lib.get_tuning("coarse_fuse") else 2 * 2)
+    assert halo[0] > 0 and coarse[0] == 2 * 2   # 2 cycles x 2 replicas
     assert smooth[0] > 0 and smooth[1] > 0
 
 
