@@ -572,13 +572,10 @@ __device__ __forceinline__ void coarse_lds_body(double *su, double *lds, double 
     const int gk = t & 31, gr = t >> 5;
     const double hh = c.h * 0.5;
     // per-point constants in registers: (f, t1, t2) = FM ? (rhs/d, v1*h/2, v2*h/2)
-    // : (rhs, v1, v2), exactly the operands the L2 version reads per use
-    auto consts = [&](long p, double &f, double &x, double &y) {
-        const double r = rhs[p], a = v1[p], b = v2[p];
-        f = FM ? r * c.rdgs : r;
-        x = FM ? a * hh : a;
-        y = FM ? b * hh : b;
-    };
+    // : (rhs, v1, v2), exactly the operands the L2 version reads per use.
+    // Every load is issued from a clamped address before any is used (the
+    // masks are applied after): one memory round trip for the set-up, not
+    // one per point branch.
     double gf[2][GP], gx[2][GP], gy[2][GP];   // colour points
     int gq[2][GP];
     bool gon[2][GP];
@@ -593,35 +590,48 @@ __device__ __forceinline__ void coarse_lds_body(double *su, double *lds, double 
             const int j = 1 + ((i + 1 + colour) & 1) + 2 * gk;
             gon[colour][p] = i <= n - 1 && j <= n - 1;
             gq[colour][p] = gon[colour][p] ? i * NP + j : NP + 1;
-            gf[colour][p] = gx[colour][p] = gy[colour][p] = 0.0;
-            if (gon[colour][p])
-                consts((long)i * pitch + j, gf[colour][p], gx[colour][p], gy[colour][p]);
+            const long q = gon[colour][p] ? (long)i * pitch + j : pitch + 1;
+            gf[colour][p] = rhs[q];
+            gx[colour][p] = v1[q];
+            gy[colour][p] = v2[q];
         }
 #pragma unroll
     for (int m = 0; m < MR; ++m) {
         const int i = 1 + ty + 16 * m, j = 1 + tx;
         ron[m] = i <= n - 1 && j <= n - 1;
         rq[m] = ron[m] ? i * NP + j : NP + 1;
-        rf[m] = rx[m] = ry[m] = 0.0;
-        if (ron[m]) consts((long)i * pitch + j, rf[m], rx[m], ry[m]);
+        const long q = ron[m] ? (long)i * pitch + j : pitch + 1;
+        rf[m] = rhs[q];
+        rx[m] = v1[q];
+        ry[m] = v2[q];
     }
+    auto scale = [&](bool on, double &f, double &x, double &y) {
+        f = on ? (FM ? f * c.rdgs : f) : 0.0;
+        x = on ? (FM ? x * hh : x) : 0.0;
+        y = on ? (FM ? y * hh : y) : 0.0;
+    };
+#pragma unroll
+    for (int colour = 0; colour < 2; ++colour)
+#pragma unroll
+        for (int p = 0; p < GP; ++p)
+            scale(gon[colour][p], gf[colour][p], gx[colour][p], gy[colour][p]);
+#pragma unroll
+    for (int m = 0; m < MR; ++m) scale(ron[m], rf[m], rx[m], ry[m]);
     {   // u into LDS: rows ty + 16m (m <= 4), columns tx, tx + 64, all loads in flight
         constexpr int MF = (kCoarseLdsMaxN + 16) / 16;
-        double a[MF][2];
+        double a[MF][2] = {};
+        if (!zero_first)   // (clamped addresses: every load in flight at once)
+#pragma unroll
+            for (int m = 0; m < MF; ++m)
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    a[m][h] = u[(long)min(ty + 16 * m, n) * pitch + min(tx + 64 * h, n)];
 #pragma unroll
         for (int m = 0; m < MF; ++m)
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int i = ty + 16 * m, j = tx + 64 * h;
-                a[m][h] = 0.0;
-                if (!zero_first && i <= n && j <= n) a[m][h] = u[(long)i * pitch + j];
-            }
-#pragma unroll
-        for (int m = 0; m < MF; ++m)
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int i = ty + 16 * m, j = tx + 64 * h;
-                if (i <= n && j <= n) su[i * NP + j] = a[m][h];
+                if (i <= n && j <= n) su[i * NP + j] = zero_first ? 0.0 : a[m][h];
             }
     }
     if (write && zero_first)   // (the row padding, as the L2 version leaves it)
