@@ -40,7 +40,10 @@ struct Level {
     int xin = -1;   // finest level: the input buffer of the last cross-cycle pass
     int nxt() const { return cur == 0 ? 1 : 0; }   // ping-pong partner of cur
     double *rhs = nullptr, *v1 = nullptr, *v2 = nullptr;
-    double *rhs_alt = nullptr;   // finest level: the next time step's rhs (step mode)
+    // finest level: the next time step's rhs (step mode); coarsest level (n <=
+    // 64, L >= 3): the rhs a W-cycle's fused pair pass restricts into while its
+    // workgroups still read the current one for the fused coarsest solve
+    double *rhs_alt = nullptr;
     // exact rank-1 factors of v1 / v2 (sepvel.h; row factors n+1, column
     // factors pitch, zero padded), or null: the passes that take them read
     // the 2-D v1 / v2 from HBM only where no factors exist
@@ -99,6 +102,10 @@ struct mgx_ctx {
     // rhs); step_spec = that state is ready for the next mgx_step
     bool step_next = false, step_spec = false;
     bool no_rhs_alt = false;   // the step-mode rhs did not fit in HBM: plain schedule
+    // tuning key "xedge_side": the cross pass's edge launch on a second stream
+    // beside its interior launch (created on first use)
+    hipStream_t xs = nullptr;
+    hipEvent_t xfork = nullptr, xjoin = nullptr;
     double step_res0 = 0;
     // profiling
     int prof = 0;   // 0 off, 1 every launch, 2 finest-level launches only
@@ -114,6 +121,15 @@ namespace mgxi {
 
 hipEvent_t take_event(mgx_ctx *c);
 
+// A launch whose lambda declined (launched nothing: the caller saw a negative
+// block count) drops the record it pushed, so profiles count real launches.
+inline void unlaunch(mgx_ctx *c, size_t pending_before) {
+    while (c->pending.size() > pending_before) {
+        c->pool.push_back(c->pending.back().e0);
+        c->pool.push_back(c->pending.back().e1);
+        c->pending.pop_back();
+    }
+}
 // Launch helper: records HIP events around the launch when profiling is on.
 // bytes: canonical algorithmic bytes of the reference ops the launch does
 // (SURVEY 8d); cbytes: its compulsory bytes (each array it must read or write,

@@ -40,19 +40,25 @@ namespace mgxi {
 
 long g_dist_min_rows = 256;
 // tuning key "dist_overlap": 1 = every partitioned level's u ghost rows are
-// exchanged on a second stream (its own communicator) as soon as the pass
-// that wrote them ends -- the pre-smoothing pass, or the finest level's cross
-// pass -- hidden behind the coarser levels of the V-cycle (the level's post
-// pass waits for it, and then exchanges only the coarser level's u for its
-// prolongation); 2 = that, and the cross pass's remaining exchange (level-1 u) on
-// the second stream too, beside the pass's interior march (the bands next to
-// the ghosts go to its edge launch); 0 = every exchange on the
-// compute stream; -1 (default) = 1 on an RCCL communicator, 0 on virtual
-// ranks.  On virtual ranks (one GPU) the early exchange's copies compete with
-// the level passes for the same chip and cost 2-3 %; over xGMI it takes the
-// level-0 exchange (2 x 16 rows, ~4 MB per rank) off the critical path for
-// nothing of the local HBM -- bench.py prices 0 / 1 / 2 on the N-GPU run
-// itself and keeps the fastest for its timed region
+// exchanged from a second stream as soon as the pass that wrote them ends --
+// the pre-smoothing pass, or the finest level's cross pass -- hidden behind
+// the coarser levels of the V-cycle (the level's post pass waits for it, and
+// then exchanges only the coarser level's u for its prolongation); 2 = that,
+// and the cross pass's remaining u ghost exchange (dist_cross: level 0's when
+// it was not exchanged early, level 1's without the communication-avoiding
+// post passes) on the second stream too, beside the pass's interior march
+// (the bands next to the ghosts go to its edge launch); 0 = every exchange on
+// the compute stream; -1
+// (default) = 1 on an RCCL communicator, 0 on virtual ranks.  The second
+// stream has NO communicator of its own: its exchanges go through the rank's
+// one communicator, chained after the previous operation by comm_op (Dist::
+// comm), so the overlap is with compute only, never between two RCCL
+// operations.  On virtual ranks (one GPU) the early exchange's copies compete
+// with the level passes for the same chip and cost 2-3 %; over xGMI it takes
+// the level-0 exchange (2 x 16 rows, ~4 MB per rank) off the critical path
+// for nothing of the local HBM -- bench.py prices 0 / 1 / 2 (with
+// dist_min_rows 128 / 256) on the N-GPU run itself and keeps the fastest for
+// its timed region
 long g_dist_overlap = -1;
 // tuning key "dist_local_side": virtual ranks (one device) run the
 // dist_overlap exchanges at their early points ON the compute stream (0,

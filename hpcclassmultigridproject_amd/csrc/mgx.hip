@@ -160,10 +160,12 @@ static mgx::VGen level_vgen(const mgx_ctx *c, int l) {
 long g_coarse_fuse = 1;
 int op_coarse(mgx_ctx *c, int l, int reps);
 // (only from a zero start, the V- and W-cycle's case after the restriction:
-// then no workgroup reads the coarse u that workgroup 0 stores at its end)
+// then no workgroup reads the coarse u that workgroup 0 stores at its end;
+// and only with nsmooth >= 1, so that the post-smoothing above is a tile pass
+// that can take it -- nsmooth 0 prolongs with op_prolong_add)
 static bool coarse_fusable(const mgx_ctx *c, int l) {
-    return g_coarse_fuse && !c->dist && c->opt.smoother == 0 && l == c->L - 1 && l >= 2 &&
-           c->lv[l].zero &&
+    return g_coarse_fuse && !c->dist && c->opt.smoother == 0 && c->opt.nsmooth >= 1 &&
+           l == c->L - 1 && l >= 2 && c->lv[l].zero &&
            c->lv[l].n <= mgx::kCoarseLdsMaxN && mgx::get_coarse_lds() &&
            c->lv[l - 1].n <= mgx::get_tile_max_n();
 }
@@ -173,6 +175,14 @@ static int flush_coarse(mgx_ctx *c) {
     const int l = c->cf_level;
     c->cf_level = -1;
     return op_coarse(c, l, c->cf_reps);
+}
+// A pass that restricts into the rhs its fused coarsest solve reads would race
+// (every workgroup loads cf.rhs at its start while others already store the
+// restriction): refuse it.  mode: the pass's kMode bits.
+static int check_coarse_rhs(const mgx::SmoothArgs &A, int mode) {
+    if (A.cf.on && (mode & mgx::kModeRestrict) && A.rhsc == A.cf.rhs)
+        return fail(MGX_E_INTERNAL, "fused coarsest solve reads the rhs its pass restricts into");
+    return MGX_OK;
 }
 // the pending coarsest solve of level l+1 into a prolongation pass of level l
 static bool take_coarse(mgx_ctx *c, int l, mgx::SmoothArgs &A) {
@@ -259,8 +269,11 @@ int op_smooth(mgx_ctx *c, int l, int sweeps, bool prolong, bool restrict_, bool 
                                          (vgu ? 0.0 : 2.0 * L.Mv()) +
                                          ((pr ? 1 : 0) + (rs ? 1 : 0)) * c->lv[l + 1].M());
             int blocks = 0;
+            CHK(check_coarse_rhs(A, mode));
+            const size_t before = c->pending.size();
             CHK(launch(c, kind, l, bytes, cbytes,
                        [&] { blocks = mgx::launch_smooth(A, k, mode, c->stream); }));
+            if (blocks < 0) unlaunch(c, before);
             if (blocks == -4 && cfuse) {
                 // the pass would march: the coarsest solve on its own, then the pass
                 // (nothing was launched)
@@ -343,6 +356,7 @@ int op_restrict(mgx_ctx *c, int l) {
 
 // u[l] += prolongation(u[l+1]) (multigrid.cpp:81-83).
 int op_prolong_add(mgx_ctx *c, int l) {
+    CHK(flush_coarse(c));   // a deferred coarsest solve must run before it is prolonged
     CHK(materialize(c, l));
     CHK(materialize(c, l + 1));
     Level &F = c->lv[l], &C = c->lv[l + 1];
@@ -361,10 +375,15 @@ int op_wpair(mgx_ctx *c, int l, bool *done) {
     *done = false;
     Level &L = c->lv[l], &Cl = c->lv[l + 1];
     const int k = c->opt.nsmooth;
-    const bool cfuse = c->cf_level == l + 1;   // the coarsest solve pending, fused
-    if (!g_wpair || c->opt.smoother != 0 || k < 1 || k > 3 || c->opt.fuse < k || L.zero ||
-        (Cl.zero && !cfuse))
+    if (!g_wpair || c->opt.smoother != 0 || k < 1 || k > 3 || c->opt.fuse < k || L.zero)
         return MGX_OK;
+    // The coarsest solve pending, fused: its workgroups read Cl.rhs at their
+    // start while the pass's restriction stores the next visit's rhs, so that
+    // goes to the level's second rhs buffer (swapped in after the launch);
+    // without one the solve runs on its own first.
+    if (c->cf_level == l + 1 && !Cl.rhs_alt) CHK(flush_coarse(c));
+    const bool cfuse = c->cf_level == l + 1;
+    if (Cl.zero && !cfuse) return MGX_OK;
     mgx::SmoothArgs A{};
     A.uin = L.u[L.cur];
     A.uout = L.u[L.nxt()];
@@ -375,21 +394,27 @@ int op_wpair(mgx_ctx *c, int l, bool *done) {
     A.pitch = L.pitch;
     A.c = L.coef;
     A.uc = Cl.U();
-    A.rhsc = Cl.rhs;
+    A.rhsc = cfuse ? Cl.rhs_alt : Cl.rhs;
     A.pitchc = Cl.pitch;
     A.partials = c->partials;
     A.norm_out = c->dscal;
     if (cfuse) take_coarse(c, l, A);
+    CHK(check_coarse_rhs(A, mgx::kModeProlong | mgx::kModeRestrict));
     // post (prolong + add, k sweeps) + pre (k sweeps, restrict)
     const double bytes = (32.0 + 40.0 * k) * L.M() + 8.0 * Cl.M() + (40.0 * k + 40.0) * L.M() +
                          24.0 * Cl.M();
     const double cbytes = 8.0 * (3.0 * L.M() + 2.0 * L.Mv() + 2.0 * Cl.M());
     int blocks = 0;
+    const size_t before = c->pending.size();
     CHK(launch(c, MGX_K_PSMOOTH, l, bytes, cbytes,
                [&] { blocks = mgx::launch_smooth_wpair(A, k, c->stream); }));
-    if (blocks == -4) return flush_coarse(c);   // nothing launched: the two passes
+    if (blocks < 0) unlaunch(c, before);   // nothing launched
+    if (blocks == -4) return flush_coarse(c);   // the two passes
     if (blocks < 0) return MGX_OK;   // a march level: the two passes as usual
-    if (cfuse) took_coarse(c, l);
+    if (cfuse) {
+        took_coarse(c, l);
+        std::swap(Cl.rhs, Cl.rhs_alt);   // the restricted rhs is the current one
+    }
     L.cur = L.nxt();
     Cl.zero = true;
     *done = true;
@@ -445,6 +470,23 @@ void drop_spec(mgx_ctx *c) {
     c->step_spec = false;
 }
 
+// tuning key "xedge_side": 1 = the cross pass's guarded edge launch (the
+// boundary strips and the top / bottom bands, ~1.7 % of the points, ~0.11 ms
+// of dependent row chains on its own at N=16384) runs on a second stream,
+// forked before the unguarded interior launch, so that its workgroups fill the
+// CUs the interior plan leaves free (246 of 256 at N=16384) instead of
+// running after it; the norm follows the join.  The two launches write
+// disjoint rows / columns from the same inputs: bitwise the same.  0 = one
+// stream, interior then edge.
+long g_xedge_side = 0;
+static int side_stream(mgx_ctx *c) {
+    if (c->xs) return MGX_OK;
+    HIPCHK(hipStreamCreateWithFlags(&c->xs, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&c->xfork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->xjoin, hipEventDisableTiming));
+    return MGX_OK;
+}
+
 // k_xsmooth on level 0: u_post (cycle k, returned by mg_outer if it stops
 // here) into one free buffer, u_pre (cycle k+1's pre-smoothing) into the
 // other, the residual of u_post -> c->dscal[0], the restriction of u_pre's
@@ -494,8 +536,27 @@ static int op_cross(mgx_ctx *c, bool store_post, bool rs = false) {
     const double cbytes = 8.0 * ((store_post ? 6.0 : 5.0) * L.M() - (L.sa1 ? 2.0 * L.M() : 0.0) +
                                  2.0 * Cl.M() + (rs ? L.M() : 0.0));
     int blocks = 0;
-    CHK(launch(c, MGX_K_XSMOOTH, 0, bytes + bytes_rs, cbytes,
-               [&] { blocks = mgx::launch_xsmooth(A, k, c->stream); }));
+    // (the split launches need the unguarded kernel: xfast on, d > 0)
+    const bool side = g_xedge_side && !rs && mgx::get_xfast() && L.coef.dgs > 0;
+    if (side) CHK(side_stream(c));
+    CHK(launch(c, MGX_K_XSMOOTH, 0, bytes + bytes_rs, cbytes, [&] {
+        if (!side) {
+            blocks = mgx::launch_xsmooth(A, k, c->stream);
+            return;
+        }
+        (void)hipEventRecord(c->xfork, c->stream);   // the pass's inputs are ready
+        A.phase = 1;   // the interior launch first, on the context stream
+        const int pm = mgx::launch_xsmooth(A, k, c->stream);
+        blocks = pm;
+        if (pm < 0) return;
+        (void)hipStreamWaitEvent(c->xs, c->xfork, 0);
+        A.phase = 3;   // the edge launch beside it, no norm
+        A.partials_done = pm;
+        blocks = mgx::launch_xsmooth(A, k, c->xs);
+        (void)hipEventRecord(c->xjoin, c->xs);
+        (void)hipStreamWaitEvent(c->stream, c->xjoin, 0);
+        if (blocks > 0) mgx::launch_xsmooth_norm(A, blocks, c->stream);
+    }));
     if (blocks < 0) return fail(MGX_E_ARG, "launch_xsmooth: unsupported sweeps / mode");
     L.xin = L.cur;
     L.cur = P;
@@ -927,6 +988,12 @@ void free_ctx(mgx_ctx *c) {
         (void)hipEventDestroy(r.e1);
     }
     for (auto e : c->pool) (void)hipEventDestroy(e);
+    if (c->xs) {
+        (void)hipStreamSynchronize(c->xs);
+        (void)hipStreamDestroy(c->xs);
+    }
+    if (c->xfork) (void)hipEventDestroy(c->xfork);
+    if (c->xjoin) (void)hipEventDestroy(c->xjoin);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1069,6 +1136,15 @@ int mgxi::create_ctx(mgx_ctx **out, long n, int maxlvl, double dt, double nu,
             if (hipMemsetAsync(*b, 0, bytes, c->stream) != hipSuccess)
                 return bail(fail(MGX_E_HIP, "hipMemset"));
         }
+    }
+    if (maxlvl >= 3 && c->lv[maxlvl - 1].n <= mgx::kCoarseLdsMaxN) {
+        // coarsest level: the second rhs of a W-cycle pair pass with the fused
+        // solve (op_wpair); zero boundary, as the restriction writes the interior
+        Level &L = c->lv[maxlvl - 1];
+        const size_t bytes = sizeof(double) * L.pitch * (L.n + 1);
+        if (hipMalloc(&L.rhs_alt, bytes) != hipSuccess ||
+            hipMemsetAsync(L.rhs_alt, 0, bytes, c->stream) != hipSuccess)
+            return bail(fail(MGX_E_HIP, "hipMalloc (coarsest rhs)"));
     }
     if (maxlvl > 1 && n >= kCrossMinN) {   // third finest-level buffer: cross-cycle pass
         Level &L = c->lv[0];
@@ -1582,6 +1658,11 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgxi::g_coarse_fuse = value;
         return MGX_OK;
     }
+    if (!strcmp(key, "xedge_side")) {
+        if (value != 0 && value != 1) return fail(MGX_E_ARG, "xedge_side must be 0 or 1");
+        mgxi::g_xedge_side = value;
+        return MGX_OK;
+    }
     if (!strcmp(key, "wpair")) {
         if (value != 0 && value != 1) return fail(MGX_E_ARG, "wpair must be 0 or 1");
         mgxi::g_wpair = value;
@@ -1708,6 +1789,10 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "wpair")) {
         *value = mgxi::g_wpair;
+        return MGX_OK;
+    }
+    if (!strcmp(key, "xedge_side")) {
+        *value = mgxi::g_xedge_side;
         return MGX_OK;
     }
     if (!strcmp(key, "dist_min_rows")) {

@@ -556,6 +556,8 @@ __global__ __launch_bounds__(MGX_TILE_THREADS) void k_smooth_tile(
     __shared__ double cred[C::PROL ? 16 : 1];
     __shared__ double cnorm;
     if constexpr (C::PROL) {
+        // (its thread layout, trip counts and 16 reduction slots are fixed)
+        static_assert(T::THREADS == 1024, "coarse_lds_body needs 1024 threads per workgroup");
         if (cf.on)
             coarse_lds_body<FM>(csu, cred, &cnorm, cf.u, cf.rhs, cf.v1, cf.v2, (int)cf.n,
                                 cf.pitch, cf.c, cf.tol, cf.maxit, cf.zero_first, cf.reps,

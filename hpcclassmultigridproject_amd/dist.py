@@ -78,7 +78,7 @@ def gather_plan(n: int, maxlvl: int, world: int, rank: int):
 
 
 def rccl_selfcheck(world: int, rank: int, device: int, n: int = 4096, maxlvl: int = 7,
-                   cycles: int = 2, group=None) -> dict:
+                   cycles: int = 2, group=None, min_rows=(), candidate_fp: str = "fma") -> dict:
     """Run libmgx's RCCL transport with real peers against a single-GPU context.
 
     Every rank builds a row-partitioned context of the same small problem
@@ -93,6 +93,11 @@ def rccl_selfcheck(world: int, rank: int, device: int, n: int = 4096, maxlvl: in
     the torch.distributed group (its backend only brokers the unique ids and
     the verdict).  -> {"bitwise": bool, "norm_rel_err": float, "modes": {overlap:
     {...}}, ...} on every rank.
+
+    min_rows: further ``dist_min_rows`` values to check (bench.py's partition
+    candidates), each with every overlap mode in the ``candidate_fp`` mode
+    only -> "candidates": {"<min_rows>:<overlap>": {...}}; a candidate the
+    bench may time has passed here first.
     """
     import numpy as np
     import torch
@@ -112,17 +117,23 @@ def rccl_selfcheck(world: int, rank: int, device: int, n: int = 4096, maxlvl: in
                 mg.rhs()
                 ref[name] = ([mg.run_cycles(1) for _ in range(cycles)], mg.download())
     # per dist_overlap mode: [bitwise so far (both fp modes), max norm error]
-    modes, la = {}, None
+    modes, las = {}, {}
+    # (dist_min_rows, overlap, fp modes): 16 in both fp modes (levels 0..5
+    # split even at world 8: every exchange of the schedule), then the bench's
+    # candidates in its own fp mode
+    runs = [(16, ov, tuple(fps)) for ov in (0, 1, 2)]
+    runs += [(mr, ov, (candidate_fp,)) for mr in min_rows if mr != 16 for ov in (0, 1, 2)]
     try:
-        _lib.set_tuning("dist_min_rows", 16)
-        for ov in (0, 1, 2):
+        for mr, ov, names in runs:
+            _lib.set_tuning("dist_min_rows", mr)
             _lib.set_tuning("dist_overlap", ov)
             ok, err = True, 0.0
-            for name, fp in fps.items():
+            for name in names:
+                fp = fps[name]
                 uid = broadcast_unique_id(group)
                 with Multigrid(n, maxlvl, dt, nu, device=device, world=world, rank=rank,
                                unique_id=uid, fp_mode=fp) as mg:
-                    la = mg.dist_info()[2]
+                    las[mr] = mg.dist_info()[2]
                     mg.upload(u0, v1, v2)
                     mg.profile(True, finest_only=True)
                     mg.rhs()
@@ -136,22 +147,26 @@ def rccl_selfcheck(world: int, rank: int, device: int, n: int = 4096, maxlvl: in
                     ok = ok and bool(np.array_equal(u, ref[name][1]))
                     err = max(err, float(np.max(np.abs(np.array(norms) - ref[name][0]) /
                                                 np.abs(ref[name][0]))))
-            modes[ov] = [ok, err]
+            modes[(mr, ov)] = [ok, err]
     finally:
         _lib.set_tuning("dist_min_rows", old_rows)
         _lib.set_tuning("dist_overlap", old_ov)
-    verdict = torch.tensor([x for ov in (0, 1, 2) for x in (1.0 if modes[ov][0] else 0.0,
-                                                             modes[ov][1])],
+    keys = [(mr, ov) for mr, ov, _ in runs]
+    verdict = torch.tensor([x for k in keys for x in (1.0 if modes[k][0] else 0.0, modes[k][1])],
                            dtype=torch.float64)
     if dist.get_backend(group) == "nccl":
         verdict = verdict.cuda()
     dist.broadcast(verdict, src=0, group=group)
     v = verdict.cpu().tolist()
-    per = {str(ov): {"bitwise": v[2 * k] == 1.0, "norm_rel_err": v[2 * k + 1],
-                     "passed": v[2 * k] == 1.0 and v[2 * k + 1] <= 1e-11}
-           for k, ov in enumerate((0, 1, 2))}
-    return {"N": n, "levels": maxlvl, "cycles": cycles, "partitioned_levels": la,
+    res = {k: {"bitwise": v[2 * i] == 1.0, "norm_rel_err": v[2 * i + 1],
+               "passed": v[2 * i] == 1.0 and v[2 * i + 1] <= 1e-11}
+           for i, k in enumerate(keys)}
+    per = {str(ov): res[(mr, ov)] for mr, ov in keys if mr == 16}
+    cand = {f"{mr}:{ov}": dict(res[(mr, ov)], partitioned_levels=las.get(mr))
+            for mr, ov in keys if mr != 16}
+    return {"N": n, "levels": maxlvl, "cycles": cycles, "partitioned_levels": las.get(16),
             "fp_modes": list(fps), "overlap": [0, 1, 2], "modes": per,
-            "bitwise": all(m["bitwise"] for m in per.values()),
-            "norm_rel_err": max(m["norm_rel_err"] for m in per.values()),
-            "passed": all(m["passed"] for m in per.values())}
+            "candidates": cand, "candidate_fp": candidate_fp,
+            "bitwise": all(m["bitwise"] for m in res.values()),
+            "norm_rel_err": max(m["norm_rel_err"] for m in res.values()),
+            "passed": all(m["passed"] for m in res.values())}

@@ -66,6 +66,7 @@ def ref(nsmooth: int = 3):
         r = _load(REF_NU2_PATH if nsmooth == 2 else REF_PATH)
         r.ref_compute_norm.restype = C.c_double
         r.ref_vcycle_once.restype = C.c_double
+        r.ref_vcycle_once_tower.restype = C.c_double
         r.ref_time_vcycles.restype = C.c_double
         _refs[nsmooth] = r
     if nsmooth == 3:

@@ -50,8 +50,13 @@ struct Tower {
 
 // Same construction as timestepper (multigrid.cpp:138-162), with calloc for the
 // coarse levels (the reference's malloc'd coarse buffers are read
-// before being written; zero-fill is the pinned semantics).
-void build(Tower &t, const double *u0, const double *v1, const double *v2, int maxlvl, int n) {
+// before being written; zero-fill is the pinned semantics).  correct = 1: the
+// CORRECT tower instead (SURVEY K2's fix, mgx's MGX_TOWER_CORRECT): level i is
+// ((n >> i) + 1)^2 and the reference's own restriction of level i-1 at its
+// true size n >> (i-1); mg_inner then reads every level at the width it was
+// built with.
+void build(Tower &t, const double *u0, const double *v1, const double *v2, int maxlvl, int n,
+           int correct = 0) {
     t.maxlvl = maxlvl;
     t.u = (double **)calloc(maxlvl + 1, sizeof(double *));
     t.rhs = (double **)calloc(maxlvl + 1, sizeof(double *));
@@ -66,12 +71,13 @@ void build(Tower &t, const double *u0, const double *v1, const double *v2, int m
     memcpy(t.v1[0], v1, cnt * sizeof(double));
     memcpy(t.v2[0], v2, cnt * sizeof(double));
     for (int i = 1; i < maxlvl; i++) {
-        int ni = (n >> 1) + 1;
+        int ni = correct ? (n >> i) + 1 : (n >> 1) + 1;
+        int nr = correct ? n >> (i - 1) : ni - 1;   // the `n` restriction is passed
         t.u[i] = (double *)calloc((size_t)ni * ni, sizeof(double));
         t.v1[i] = (double *)calloc((size_t)ni * ni, sizeof(double));
-        restriction(t.v1[i], t.v1[i - 1], ni - 1);
+        restriction(t.v1[i], t.v1[i - 1], nr);
         t.v2[i] = (double *)calloc((size_t)ni * ni, sizeof(double));
-        restriction(t.v2[i], t.v2[i - 1], ni - 1);
+        restriction(t.v2[i], t.v2[i - 1], nr);
         t.rhs[i] = (double *)calloc((size_t)ni * ni, sizeof(double));
     }
     t.tmp = (double *)calloc(cnt, sizeof(double));
@@ -128,10 +134,10 @@ void ref_timestepper(double *uT, double *u0, double *v1, double *v2, double nu, 
 // One reference V-cycle (mg_inner) on a fresh tower built from (u, v1, v2) with
 // rhs = compute_rhs(u) (multigrid.cpp:167); u is updated in place.  Returns the
 // norm of the residual after the cycle (multigrid.cpp:112-113).
-double ref_vcycle_once(double *u, double *v1, double *v2, int n, int maxlvl, double dt,
-                       double nu, int shape, int nthreads) {
+double ref_vcycle_once_tower(double *u, double *v1, double *v2, int n, int maxlvl, double dt,
+                             double nu, int shape, int nthreads, int correct) {
     Tower t;
-    build(t, u, v1, v2, maxlvl, n);
+    build(t, u, v1, v2, maxlvl, n, correct);
     double dx = 1.0 / n, res = 0.0;
     run_threads(nthreads, [&] {
         compute_rhs(t.rhs[0], t.u[0], n, t.v1[0], t.v2[0], dt, nu, dx);
@@ -142,6 +148,10 @@ double ref_vcycle_once(double *u, double *v1, double *v2, int n, int maxlvl, dou
     memcpy(u, t.u[0], (size_t)(n + 1) * (n + 1) * sizeof(double));
     release(t);
     return res;
+}
+double ref_vcycle_once(double *u, double *v1, double *v2, int n, int maxlvl, double dt,
+                       double nu, int shape, int nthreads) {
+    return ref_vcycle_once_tower(u, v1, v2, n, maxlvl, dt, nu, shape, nthreads, 0);
 }
 
 // CPU baseline: `cycles` timed V-cycles (mg_inner + residual + compute_norm, the

@@ -103,21 +103,34 @@ def e2e_fixture(N, nu, tag, summary):
     summary["e2e"][tag] = s
 
 
-def vcycle_fixture(N, maxlvl, nthreads, tag, summary, keep_full=False):
+def vcycle_fixture(N, maxlvl, nthreads, tag, summary, keep_full=False, tower=0):
+    """One reference V-cycle; tower 1 = the correct velocity tower, built by
+    the reference's own restriction at each level's true size
+    (oracle/ref_harness.cpp build, correct = 1)."""
     u0, v1, v2 = O.init_problem(N)
     dt = 1.0 / N / 10
     u = u0.copy()
     t = time.time()
-    res = O.ref().ref_vcycle_once(p(u), p(v1), p(v2), I(N), I(maxlvl), D(dt), D(NU), I(1),
-                                  I(nthreads))
+    res = O.ref().ref_vcycle_once_tower(p(u), p(v1), p(v2), I(N), I(maxlvl), D(dt), D(NU),
+                                        I(1), I(nthreads), I(tower))
     s = stats(u, N)
     s.update({"maxlvl": maxlvl, "nsmooth": 3, "res_after": repr(res), "nthreads": nthreads,
+              "tower": "correct" if tower else "reference",
               "ref_seconds": round(time.time() - t, 2)})
     summary["vcycle"][tag] = s
     data = {"sample": strided(u, N), "params": np.array([N, maxlvl, NU, dt])}
     if keep_full:
         data["u"] = u
     np.savez_compressed(os.path.join(HERE, f"vcycle_{tag}.npz"), **data)
+
+
+def correct_tower_fixtures(summary, large=True):
+    """The correct velocity tower (every level injected from the one above at
+    its true size) through the reference's own restriction and mg_inner: one
+    V-cycle at N=4096, L=7 and (large) at the headline size N=16384, L=9."""
+    vcycle_fixture(4096, 7, 8, "N4096_L7_correct", summary, tower=1)
+    if large:
+        vcycle_fixture(16384, 9, 8, "N16384_L9_correct", summary, tower=1)
 
 
 def config2_fixture(summary, nthreads=8):
@@ -170,6 +183,9 @@ def main():
     ap.add_argument("--large", action="store_true")
     ap.add_argument("--only-config2", action="store_true",
                     help="add the config-2 (NITER=2) fixtures to summary.json and stop")
+    ap.add_argument("--only-correct-tower", action="store_true",
+                    help="add the correct-tower V-cycle fixtures (N=4096 L=7 and N=16384 "
+                         "L=9) to summary.json and stop")
     args = ap.parse_args()
     if not O.ref_available():
         sys.exit("oracle/_ref/libmgref.so missing: build with `make -C oracle` here")
@@ -179,8 +195,11 @@ def main():
     summary.setdefault("vcycle", {})
     summary.setdefault("steps", {})
     summary["generator"] = "tests/golden/make_golden.py (reference compiled by oracle/Makefile)"
-    if args.only_config2:
-        config2_fixture(summary)
+    if args.only_config2 or args.only_correct_tower:
+        if args.only_config2:
+            config2_fixture(summary)
+        else:
+            correct_tower_fixtures(summary)
         with open(path, "w") as f:
             json.dump(summary, f, indent=1, sort_keys=True)
         return
@@ -193,6 +212,7 @@ def main():
     vcycle_fixture(1024, 6, 8, "N1024_L6", summary)
     vcycle_fixture(4096, 3, 8, "N4096_L3", summary)
     config2_fixture(summary)
+    correct_tower_fixtures(summary, large=args.large)
     if args.large:
         vcycle_fixture(16384, 9, 8, "N16384_L9", summary)
         large_steps(16384, 9, 2, 8, summary)

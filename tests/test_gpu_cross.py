@@ -124,6 +124,28 @@ def test_unguarded_interior_kernel_equals_guarded(N, L, G, xt, cross, knobs):
     np.testing.assert_allclose(n1, n0, rtol=NORM_RTOL)
 
 
+@pytest.mark.parametrize("N,L,fp", [(8192, 5, _lib.FP_FMA), (4096, 6, _lib.FP_BITWISE),
+                                    (16384, 9, _lib.FP_FMA)], ids=["N8192fma", "N4096", "N16384fma"])
+def test_edge_launch_on_side_stream_equals_one_stream(N, L, fp, cross, knobs):
+    """xedge_side: the cross pass's guarded edge launch on a second stream
+    beside the interior launch (disjoint outputs from the same inputs, the
+    norm after the join) -- u and the norms bitwise the one-stream pass, for
+    single cycles (u_post stored) and a batch, and inside mg_outer."""
+    cross(1)
+    out = []
+    u0, v1, v2 = init_problem(N)
+    for v in (0, 1):
+        knobs(xedge_side=v)
+        with Multigrid(N, L, 1.0 / N / 10, NU, fp_mode=fp) as mg:
+            mg.upload(u0, v1, v2)
+            mg.rhs()
+            norms = [mg.run_cycles(1) for _ in range(2)] + [mg.run_cycles(3)]
+            cyc = mg.step(1e-6)
+            out.append((mg.download(), norms, cyc))
+    assert np.array_equal(out[0][0], out[1][0])
+    assert out[0][1] == out[1][1] and out[0][2] == out[1][2]
+
+
 @pytest.mark.parametrize("store_post", [False, True], ids=["pre_only", "post_too"])
 def test_edge_tiles_store_post_vs_checker(store_post, cross, knobs, oracle_mod):
     """The edge tiles also write u_post when the cycle's solution is observed
@@ -232,6 +254,54 @@ def test_coarse_fuse_equals_separate_launch(N, L, shape, fp, parts, knobs):
     if za is not None:
         assert np.array_equal(za, zb)
     assert la > 0 and lb == 0
+
+
+@pytest.mark.parametrize("shape", [1, 2], ids=["V", "W"])
+def test_coarse_fuse_nsmooth0_vs_oracle(shape, knobs, oracle_mod):
+    """nsmooth = 0 (no smoothing, multigrid.cpp:69-88 with NITER 0): the
+    prolongation is op_prolong_add, not a tile pass, so the coarsest solve must
+    not be deferred into it -- coarse_fuse 0 and 1 bitwise equal, and equal to
+    the CPU checker's mg_inner (advisor finding: with the solve deferred, the
+    prolongation used to read the unsolved, zero coarse u)."""
+    N, L = 1024, 5   # coarsest n = 64
+    dt = 1.0 / N / 10
+    u0, v1, v2 = init_problem(N)
+    out = []
+    for v in (0, 1):
+        knobs(coarse_fuse=v)
+        with Multigrid(N, L, dt, NU, shape=shape, nsmooth=0) as mg:
+            mg.upload(u0, v1, v2)
+            mg.rhs()
+            for _ in range(2):
+                mg.mg_inner()
+            out.append((mg.download(), mg.coarse_iterations()))
+    assert np.array_equal(out[0][0], out[1][0]) and out[0][1] == out[1][1]
+    O = oracle_mod
+    O.set_threads(8)
+    t = O.Tower(u0, v1, v2, N, L)
+    O.compute_rhs(t.ufine, N, v1, v2, dt, NU, 1.0 / N, rhs=t.rhsfine)
+    for _ in range(2):
+        t.mg_inner(dt, NU, shape=shape, nsmooth=0)
+    assert np.array_equal(out[1][0], t.ufine)
+    assert not np.array_equal(out[1][0], u0)   # the correction was applied
+
+
+def test_wcycle_profile_counts_only_real_launches(knobs):
+    """A W-cycle's pair pass declines on march levels (nothing launched); the
+    profile must not count it: level 0 (n = 2048, a row march) runs exactly
+    `shape` post-smoothing passes per cycle."""
+    knobs(wpair=1)
+    N, L = 2048, 6
+    u0, v1, v2 = init_problem(N)
+    with Multigrid(N, L, 1.0 / N / 10, NU, shape=2) as mg:
+        mg.upload(u0, v1, v2)
+        mg.rhs()
+        mg.profile(True)
+        for _ in range(2):
+            mg.mg_inner()
+        n0 = mg.profile_get(_lib.K_PSMOOTH, 0)[0]
+        mg.profile(False)
+    assert n0 == 2 * 2, n0
 
 
 def test_negative_diagonal_routes_to_general_division(cross, oracle_mod):

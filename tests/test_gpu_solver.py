@@ -89,6 +89,38 @@ def test_vcycle_bitwise_vs_reference_N16384(golden_summary):
         assert np.array_equal(u.reshape(N + 1, N + 1)[::step, ::step], g["sample"])
 
 
+@pytest.mark.parametrize("tag", ["N4096_L7_correct", "N16384_L9_correct"])
+def test_vcycle_correct_tower_vs_reference(golden_summary, tag):
+    """TOWER_CORRECT (every coarse velocity level injected from the one
+    above at its true size; the tower every row-block and N > 16384 run uses)
+    at the headline size: one V-cycle bitwise equal to the compiled
+    reference's mg_inner on the same tower (sha256 and the 65x65 sample,
+    tests/golden/make_golden.py correct_tower_fixtures); the fma mode within
+    SURVEY K3's 1e-12 of it, same residual to 1e-9 relative."""
+    s = golden_summary["vcycle"][tag]
+    N, maxlvl = s["N"], s["maxlvl"]
+    u0, v1, v2 = init_problem(N)
+    dt = 1.0 / N / 10
+    out = {}
+    for fp in (_lib.FP_BITWISE, _lib.FP_FMA):
+        with Multigrid(N, maxlvl, dt, NU, tower_mode=_lib.TOWER_CORRECT, fp_mode=fp) as mg:
+            mg.upload(u0, v1, v2)
+            mg.rhs()
+            mg.mg_inner()
+            out[fp] = (mg.download(), mg.residual_norm(0))
+    ub, rb = out[_lib.FP_BITWISE]
+    assert hashlib.sha256(ub.tobytes()).hexdigest() == s["sha256"]
+    g = load_golden(f"vcycle_{tag}.npz")
+    step = N // 64
+    assert np.array_equal(ub.reshape(N + 1, N + 1)[::step, ::step], g["sample"])
+    # the norm differs only by summation order: the reference sums (N-1)^2
+    # squares serially (2.7e8 at N=16384; measured 2.8e-11 relative there)
+    assert abs(rb - float(s["res_after"])) <= 1e-10 * float(s["res_after"])
+    uf, rf = out[_lib.FP_FMA]
+    assert float(np.max(np.abs(uf - ub))) <= 1e-12
+    assert abs(rf - rb) <= 1e-9 * rb
+
+
 @pytest.mark.slow
 def test_two_timesteps_N16384(golden_summary):
     s = golden_summary["steps"].get("N16384_L9_2steps")

@@ -59,12 +59,14 @@ def test_vcycle_larger_matches_reference_summary(oracle_mod, golden_summary):
     O = oracle_mod
     O.set_threads(4)
     try:
-        for tag in ("N1024_L6", "N4096_L3"):
+        # (N4096_L7_correct: the correct velocity tower, built by the
+        # reference's own restriction at every level's true size)
+        for tag in ("N1024_L6", "N4096_L3", "N4096_L7_correct"):
             s = golden_summary["vcycle"][tag]
             N, maxlvl = s["N"], s["maxlvl"]
             u0, v1, v2 = O.init_problem(N)
             dt = 1.0 / N / 10
-            t = O.Tower(u0, v1, v2, N, maxlvl)
+            t = O.Tower(u0, v1, v2, N, maxlvl, 1 if s.get("tower") == "correct" else 0)
             O.compute_rhs(t.ufine, N, v1, v2, dt, NU, 1.0 / N, rhs=t.rhsfine)
             t.mg_inner(dt, NU)
             assert hashlib.sha256(t.ufine.tobytes()).hexdigest() == s["sha256"], tag
