@@ -257,7 +257,7 @@ class GpuState:
         return out
 
 
-MIN_ROWS_CANDIDATES = (128, 256)   # dist_min_rows priced by the N > 1 warm-up
+MIN_ROWS_CANDIDATES = (128, 256, 512)   # dist_min_rows priced by the N > 1 warm-up
 DEFAULT_MIN_ROWS = 256
 
 
@@ -287,6 +287,39 @@ def pricing_candidates(overlap_arg, min_rows_arg, N, rccl_check):
                     continue
             cands.append((r, ov))
     return cands or [(DEFAULT_MIN_ROWS, 0)]
+
+
+def price_partitions(mg, cur_rows, cands, make_ctx, barrier, max_over_ranks, set_overlap,
+                     cycles=3):
+    """Time `cycles` warm-up cycles (max over ranks) per (dist_min_rows,
+    dist_overlap) candidate; a context is rebuilt (make_ctx(rows, 1)) only when
+    the rows change -- rows descending, so the first is `mg`'s own when it was
+    built with the largest -- and once more for the winner if needed.
+    -> (context of the winner, its rows, best rows, best overlap,
+    {"rows:overlap": ms per cycle})."""
+    ab = {}
+    for r in sorted({r for r, _ in cands}, reverse=True):
+        if r != cur_rows:
+            mg.close()
+            mg = make_ctx(r, 1)
+            cur_rows = r
+        for rr, ov in cands:
+            if rr != r:
+                continue
+            set_overlap(ov)
+            mg.run_cycles(1)
+            mg.synchronize()
+            barrier()
+            t0 = time.perf_counter()
+            mg.run_cycles(cycles)
+            mg.synchronize()
+            ab[f"{r}:{ov}"] = round(max_over_ranks(time.perf_counter() - t0) / cycles * 1e3, 4)
+    best_rows, best_ov = min(cands, key=lambda c: ab[f"{c[0]}:{c[1]}"])
+    if best_rows != cur_rows:
+        mg.close()
+        mg = make_ctx(best_rows, 1)
+        cur_rows = best_rows
+    return mg, cur_rows, best_rows, best_ov, ab
 
 
 class Watchdog:
@@ -545,31 +578,10 @@ def main():
         # exchange per cycle); only pairs whose RCCL
         # self-check passed bitwise are candidates
         if len(cands) > 1:
-            overlap_ab = {}
-            wd = watch("partition / overlap pricing").__enter__()
-            for r in sorted({r for r, _ in cands}, reverse=True):
-                if r != cur_rows:
-                    mg.close()
-                    mg = make_ctx(r, 1)
-                    cur_rows = r
-                for rr, ov in cands:
-                    if rr != r:
-                        continue
-                    _lib.set_tuning("dist_overlap", ov)
-                    mg.run_cycles(1)
-                    mg.synchronize()
-                    barrier()
-                    t0 = time.perf_counter()
-                    mg.run_cycles(3)
-                    mg.synchronize()
-                    overlap_ab[f"{r}:{ov}"] = round(
-                        max_over_ranks(time.perf_counter() - t0) / 3 * 1e3, 4)
-            best_rows, best_ov = min(cands, key=lambda c: overlap_ab[f"{c[0]}:{c[1]}"])
-            if best_rows != cur_rows:
-                mg.close()
-                mg = make_ctx(best_rows, 1)
-                cur_rows = best_rows
-            wd.__exit__(None, None, None)
+            with watch("partition / overlap pricing"):
+                mg, cur_rows, best_rows, best_ov, overlap_ab = price_partitions(
+                    mg, cur_rows, cands, make_ctx, barrier, max_over_ranks,
+                    lambda ov: _lib.set_tuning("dist_overlap", ov))
         else:
             best_rows, best_ov = cands[0]
         _lib.set_tuning("dist_overlap", best_ov)
@@ -773,6 +785,7 @@ def main():
     fp_name = "fma" if fp == _lib.FP_FMA else "bitwise"
     other = None
     generic = None
+    nonrank1 = None
     correct = None
     if world == 1 and not args.no_compare:
         # the other arithmetic mode (bitwise: every value the reference's)
@@ -785,6 +798,13 @@ def main():
         # coarser levels' all-zero velocity rows
         generic = side_run("generic velocity", fp, {"sep_velocity": 0, "zero_rows": 0}, 3)
         generic["note"] = "sep_velocity=0, zero_rows=0: every velocity row read from HBM"
+        # a velocity field that is not an exact rank-1 product (any user
+        # field): no factors, so no generator either, but the reference
+        # tower's all-zero coarse rows (whatever the field) still
+        # come from the zero row -- what such a field runs at
+        nonrank1 = side_run("non-rank-1 velocity field", fp, {"sep_velocity": 0}, 3)
+        nonrank1["note"] = ("sep_velocity=0 (factors and vgen off); zero_rows on: the "
+                            "reference tower's zero coarse rows hold for any field")
         if tower == pkg._lib.TOWER_REFERENCE:
             # the correct velocity tower (SURVEY K2's fix; what every row-block
             # and N > 16384 run uses): levels 1..L-2 generate their velocity
@@ -867,6 +887,7 @@ def main():
                     if world == 1 else None,
         "other_fp_mode": other,
         "generic_velocity_path": generic,
+        "non_rank1_velocity": nonrank1,
         "correct_tower": correct,
     }
     # what the loaded library was built from (csrc/Makefile stamps it): the

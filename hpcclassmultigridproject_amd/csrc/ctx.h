@@ -102,10 +102,6 @@ struct mgx_ctx {
     // rhs); step_spec = that state is ready for the next mgx_step
     bool step_next = false, step_spec = false;
     bool no_rhs_alt = false;   // the step-mode rhs did not fit in HBM: plain schedule
-    // tuning key "xedge_side": the cross pass's edge launch on a second stream
-    // beside its interior launch (created on first use)
-    hipStream_t xs = nullptr;
-    hipEvent_t xfork = nullptr, xjoin = nullptr;
     double step_res0 = 0;
     // profiling
     int prof = 0;   // 0 off, 1 every launch, 2 finest-level launches only

@@ -190,16 +190,10 @@ struct XArgs {
     // rows [ra, ra+band) and [rb-band, rb) from the unguarded interior march to
     // the edge launch; phase 1 = the interior march only (returns its partials
     // count, no norm), phase 2 = the edge launch only, its partials written
-    // after the first `partials_done` and the norm taken over both; phase 3 =
-    // phase 2 without the norm (returns the partials count of both launches:
-    // launch_xsmooth_norm takes it after the two are joined; the concurrent
-    // edge launch, tuning key "xedge_side"); 0 = both.
+    // after the first `partials_done` and the norm taken over both; 0 = both.
     int band = 0, phase = 0, partials_done = 0;
 };
 int launch_xsmooth(const XArgs &a, int sweeps, hipStream_t s);
-// the norm(s) of a cross pass over its `blocks` partials (launch_xsmooth's
-// last step; separately after a phase-3 launch)
-void launch_xsmooth_norm(const XArgs &a, int blocks, hipStream_t s);
 // whether launch_xsmooth supports rhs_next on a whole level of size n
 bool xstep_supported(long n);
 // Cross pass: 1 = interior strips run the unguarded march (default), 0 = all guarded.

@@ -470,23 +470,6 @@ void drop_spec(mgx_ctx *c) {
     c->step_spec = false;
 }
 
-// tuning key "xedge_side": 1 = the cross pass's guarded edge launch (the
-// boundary strips and the top / bottom bands, ~1.7 % of the points, ~0.11 ms
-// of dependent row chains on its own at N=16384) runs on a second stream,
-// forked before the unguarded interior launch, so that its workgroups fill the
-// CUs the interior plan leaves free (246 of 256 at N=16384) instead of
-// running after it; the norm follows the join.  The two launches write
-// disjoint rows / columns from the same inputs: bitwise the same.  0 = one
-// stream, interior then edge.
-long g_xedge_side = 0;
-static int side_stream(mgx_ctx *c) {
-    if (c->xs) return MGX_OK;
-    HIPCHK(hipStreamCreateWithFlags(&c->xs, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&c->xfork, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&c->xjoin, hipEventDisableTiming));
-    return MGX_OK;
-}
-
 // k_xsmooth on level 0: u_post (cycle k, returned by mg_outer if it stops
 // here) into one free buffer, u_pre (cycle k+1's pre-smoothing) into the
 // other, the residual of u_post -> c->dscal[0], the restriction of u_pre's
@@ -536,27 +519,8 @@ static int op_cross(mgx_ctx *c, bool store_post, bool rs = false) {
     const double cbytes = 8.0 * ((store_post ? 6.0 : 5.0) * L.M() - (L.sa1 ? 2.0 * L.M() : 0.0) +
                                  2.0 * Cl.M() + (rs ? L.M() : 0.0));
     int blocks = 0;
-    // (the split launches need the unguarded kernel: xfast on, d > 0)
-    const bool side = g_xedge_side && !rs && mgx::get_xfast() && L.coef.dgs > 0;
-    if (side) CHK(side_stream(c));
-    CHK(launch(c, MGX_K_XSMOOTH, 0, bytes + bytes_rs, cbytes, [&] {
-        if (!side) {
-            blocks = mgx::launch_xsmooth(A, k, c->stream);
-            return;
-        }
-        (void)hipEventRecord(c->xfork, c->stream);   // the pass's inputs are ready
-        A.phase = 1;   // the interior launch first, on the context stream
-        const int pm = mgx::launch_xsmooth(A, k, c->stream);
-        blocks = pm;
-        if (pm < 0) return;
-        (void)hipStreamWaitEvent(c->xs, c->xfork, 0);
-        A.phase = 3;   // the edge launch beside it, no norm
-        A.partials_done = pm;
-        blocks = mgx::launch_xsmooth(A, k, c->xs);
-        (void)hipEventRecord(c->xjoin, c->xs);
-        (void)hipStreamWaitEvent(c->stream, c->xjoin, 0);
-        if (blocks > 0) mgx::launch_xsmooth_norm(A, blocks, c->stream);
-    }));
+    CHK(launch(c, MGX_K_XSMOOTH, 0, bytes + bytes_rs, cbytes,
+               [&] { blocks = mgx::launch_xsmooth(A, k, c->stream); }));
     if (blocks < 0) return fail(MGX_E_ARG, "launch_xsmooth: unsupported sweeps / mode");
     L.xin = L.cur;
     L.cur = P;
@@ -988,12 +952,6 @@ void free_ctx(mgx_ctx *c) {
         (void)hipEventDestroy(r.e1);
     }
     for (auto e : c->pool) (void)hipEventDestroy(e);
-    if (c->xs) {
-        (void)hipStreamSynchronize(c->xs);
-        (void)hipStreamDestroy(c->xs);
-    }
-    if (c->xfork) (void)hipEventDestroy(c->xfork);
-    if (c->xjoin) (void)hipEventDestroy(c->xjoin);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1658,11 +1616,6 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
         mgxi::g_coarse_fuse = value;
         return MGX_OK;
     }
-    if (!strcmp(key, "xedge_side")) {
-        if (value != 0 && value != 1) return fail(MGX_E_ARG, "xedge_side must be 0 or 1");
-        mgxi::g_xedge_side = value;
-        return MGX_OK;
-    }
     if (!strcmp(key, "wpair")) {
         if (value != 0 && value != 1) return fail(MGX_E_ARG, "wpair must be 0 or 1");
         mgxi::g_wpair = value;
@@ -1789,10 +1742,6 @@ extern "C" int mgx_get_tuning(const char *key, long *value) {
     }
     if (!strcmp(key, "wpair")) {
         *value = mgxi::g_wpair;
-        return MGX_OK;
-    }
-    if (!strcmp(key, "xedge_side")) {
-        *value = mgxi::g_xedge_side;
         return MGX_OK;
     }
     if (!strcmp(key, "dist_min_rows")) {

@@ -1000,13 +1000,8 @@ static int xsmooth_inst(const XArgs &A, hipStream_t s) {
     return pm + pe;
 }
 
-int launch_xsmooth(const XArgs &A0, int sweeps, hipStream_t s) {
-    if (A0.rb >= 0 && (A0.ra & 1)) return -1;   // row blocks start at even rows
-    // phase 3: the edge launch of phase 2 without the norm (launch_xsmooth_norm
-    // takes it once both launches are joined)
-    XArgs A = A0;
-    const bool no_norm = A.phase == 3;
-    if (no_norm) A.phase = 2;
+int launch_xsmooth(const XArgs &A, int sweeps, hipStream_t s) {
+    if (A.rb >= 0 && (A.ra & 1)) return -1;   // row blocks start at even rows
     int blocks = -1;
     // 4 strip pairs per workgroup (one workgroup of 8 waves per CU): adjacent
     // 1-KiB row pieces of four strips per load (measured: 4.05 ms vs 4.13 ms
@@ -1016,16 +1011,12 @@ int launch_xsmooth(const XArgs &A0, int sweeps, hipStream_t s) {
         case 3: blocks = xsmooth_inst<4, 3>(A, s); break;
         default: return -1;
     }
-    if (A.phase == 1 || no_norm) return blocks;   // the norm comes with phase 2
-    launch_xsmooth_norm(A, blocks, s);
-    return blocks;
-}
-
-void launch_xsmooth_norm(const XArgs &A, int blocks, hipStream_t s) {
+    if (A.phase == 1) return blocks;   // the norm comes with phase 2
     if (blocks > 0)
         launch_norm_final(A.partials, blocks, A.norm_out, A.norm_accumulate ? 2 : A.norm_sqrt ? 1 : 0, s);
     if (blocks > 0 && A.rhs_next)   // the next step's initial norm
         launch_norm_final(A.partials + kNormBlocks, blocks, A.norm2_out, 1, s);
+    return blocks;
 }
 
 bool xstep_supported(long n) {

@@ -15,13 +15,13 @@ def _check(fail=(), base_fail=()):
     """A self-check verdict: min_rows 16 per overlap, candidates per pair."""
     modes = {str(ov): {"passed": str(ov) not in base_fail} for ov in (0, 1, 2)}
     cand = {f"{r}:{ov}": {"passed": f"{r}:{ov}" not in fail}
-            for r in (128, 256) for ov in (0, 1, 2)}
+            for r in (128, 256, 512) for ov in (0, 1, 2)}
     return {"modes": modes, "candidates": cand}
 
 
 def test_candidate_set_at_the_headline_size():
     c = bench.pricing_candidates("auto", "auto", 16384, None)
-    assert c == [(128, 0), (128, 1), (128, 2), (256, 0), (256, 1), (256, 2)]
+    assert c == [(r, ov) for r in (128, 256, 512) for ov in (0, 1, 2)]
     # the rows the self-check must cover are exactly these
     assert sorted({r for r, _ in c}) == list(bench.MIN_ROWS_CANDIDATES)
 
@@ -38,12 +38,12 @@ def test_fixed_arguments():
 
 def test_failed_self_check_pairs_are_dropped():
     c = bench.pricing_candidates("auto", "auto", 16384, _check(fail=("128:2", "256:0")))
-    assert (128, 2) not in c and (256, 0) not in c and len(c) == 4
+    assert (128, 2) not in c and (256, 0) not in c and len(c) == 7
     # an overlap mode whose min_rows 16 check failed is dropped for every rows value
     c = bench.pricing_candidates("auto", "auto", 16384, _check(base_fail=("1",)))
-    assert all(ov != 1 for _, ov in c) and len(c) == 4
+    assert all(ov != 1 for _, ov in c) and len(c) == 6
 
 
 def test_never_empty():
-    every = tuple(f"{r}:{ov}" for r in (128, 256) for ov in (0, 1, 2))
+    every = tuple(f"{r}:{ov}" for r in (128, 256, 512) for ov in (0, 1, 2))
     assert bench.pricing_candidates("auto", "auto", 16384, _check(fail=every)) == [(256, 0)]

@@ -124,28 +124,6 @@ def test_unguarded_interior_kernel_equals_guarded(N, L, G, xt, cross, knobs):
     np.testing.assert_allclose(n1, n0, rtol=NORM_RTOL)
 
 
-@pytest.mark.parametrize("N,L,fp", [(8192, 5, _lib.FP_FMA), (4096, 6, _lib.FP_BITWISE),
-                                    (16384, 9, _lib.FP_FMA)], ids=["N8192fma", "N4096", "N16384fma"])
-def test_edge_launch_on_side_stream_equals_one_stream(N, L, fp, cross, knobs):
-    """xedge_side: the cross pass's guarded edge launch on a second stream
-    beside the interior launch (disjoint outputs from the same inputs, the
-    norm after the join) -- u and the norms bitwise the one-stream pass, for
-    single cycles (u_post stored) and a batch, and inside mg_outer."""
-    cross(1)
-    out = []
-    u0, v1, v2 = init_problem(N)
-    for v in (0, 1):
-        knobs(xedge_side=v)
-        with Multigrid(N, L, 1.0 / N / 10, NU, fp_mode=fp) as mg:
-            mg.upload(u0, v1, v2)
-            mg.rhs()
-            norms = [mg.run_cycles(1) for _ in range(2)] + [mg.run_cycles(3)]
-            cyc = mg.step(1e-6)
-            out.append((mg.download(), norms, cyc))
-    assert np.array_equal(out[0][0], out[1][0])
-    assert out[0][1] == out[1][1] and out[0][2] == out[1][2]
-
-
 @pytest.mark.parametrize("store_post", [False, True], ids=["pre_only", "post_too"])
 def test_edge_tiles_store_post_vs_checker(store_post, cross, knobs, oracle_mod):
     """The edge tiles also write u_post when the cycle's solution is observed

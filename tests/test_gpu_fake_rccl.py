@@ -52,10 +52,12 @@ def _scenarios():
     # fp_mode fma: bitwise the one-GPU fma context (partition-independent forms)
     sc.append(dict(N=4096, L=7, world=4, min_rows=16, overlap=1, fp="fma", full_download=True))
     sc.append(dict(N=16384, L=9, world=8, overlap=2, fp="fma"))
-    # bench.py's other partition candidate (dist_min_rows 128: level 4 split
-    # as well, la = 5 at world 8), every overlap mode, in the bench's fma mode
-    for ov in (0, 1, 2):
-        sc.append(dict(N=16384, L=9, world=8, min_rows=128, overlap=ov, fp="fma"))
+    # bench.py's other partition candidates (dist_min_rows 128: level 4 split
+    # as well, la = 5 at world 8; 512: levels 0-2 only, la = 3), every overlap
+    # mode, in the bench's fma mode
+    for mr in (128, 512):
+        for ov in (0, 1, 2):
+            sc.append(dict(N=16384, L=9, world=8, min_rows=mr, overlap=ov, fp="fma"))
     # the negative case: dist.hip's operation chain dropped (test hook) -- the
     # side stream's early exchanges and the compute stream's collectives are
     # then unordered, and the fake's happens-before check must say so
@@ -148,7 +150,7 @@ def test_rccl_branch_with_thread_peers_bitwise_vs_one_gpu(tmp_path):
             assert ph == v["ref_phase_xsmooth"], (sc, r, ph, v["ref_phase_xsmooth"])
         assert v["replicated_level"] >= 2, sc
         if sc["N"] == 16384 and sc["world"] == 8:   # the partition the candidates set
-            assert v["replicated_level"] == {128: 5, 256: 4}[sc.get("min_rows", 256)], sc
+            assert v["replicated_level"] == {128: 5, 256: 4, 512: 3}[sc.get("min_rows", 256)], sc
         _assert_call_counts(v)
         # after mgx_synchronize no RCCL operation of the rank is in flight
         # (a caller's own collectives may follow: bench.py's barriers)
