@@ -102,6 +102,13 @@ __device__ __forceinline__ const char *rowb(const double *row, unsigned boff) {
 __device__ __forceinline__ double2 ld2u(const double *row, unsigned boff) {
     return *reinterpret_cast<const double2 *>(rowb(row, boff));
 }
+// two consecutive doubles from an address that is only 8-B aligned (one
+// 16-B global load: the coarsest solve's column pairs start at odd columns)
+__device__ __forceinline__ double2 ldu2(const double *p) {
+    typedef double d2a8 __attribute__((ext_vector_type(2), aligned(8)));
+    const d2a8 v = *reinterpret_cast<const d2a8 *>(p);
+    return make_double2(v.x, v.y);
+}
 __device__ __forceinline__ double ld1u(const double *row, unsigned boff) {
     return *reinterpret_cast<const double *>(rowb(row, boff));
 }
@@ -538,15 +545,20 @@ unsigned plan_march(const MarchRegions &reg, int wpb, long slots, long min_rows,
 // norms and the iteration count are bitwise those of k_coarse_solve.
 //
 // Latency and LDS issue, not work, are the cost of this kernel (~4 K points):
-//   * the colour stages map the 1024 threads onto the colour's points as
-//     (row 1 + (t >> 5) + 32p, the colour's column 2(t & 31) + 1 or + 2): two
-//     points per thread, every lane busy (k_coarse_solve's layout leaves half
-//     the lanes idle and gives the others four rows each), and each stage
-//     first reads the neighbours of both points, then stores both updates
-//     (the points of a colour are independent);
-//   * the residual keeps k_coarse_solve's layout (rows 1 + ty + 16m, column
-//     1 + tx) and its summation order (rows m ascending, then the wave
-//     butterfly, then the 16 waves in order), so the norms are its bits;
+//   * the 1024 threads map onto the interior as (row 1 + (t >> 5) + 32p,
+//     columns 2(t & 31) + 1 and + 2): four points per thread, two of each
+//     colour, every lane busy; a colour stage first reads the neighbours of
+//     its two points, then stores both updates (the points of a colour are
+//     independent);
+//   * the set-up loads each row's column pair of rhs / v1 / v2 as ONE 16-B
+//     load (6 per thread instead of 24 scalar loads of the earlier layout,
+//     whose separate residual points needed their own copies), all in flight
+//     at once from clamped addresses, masks applied after;
+//   * the residual runs on the same four points from the same registers and
+//     is summed in a fixed order (p, then colour; then the wave butterfly,
+//     then the 16 wave partials in order, by EVERY thread, so the norm needs
+//     no broadcast barrier): three barriers per iteration (two colour stages,
+//     the partials) instead of five;
 //   * every loop is unrolled to its fixed trip count for n <= 64, guarded.
 // reps: the solve repeated back to back (a W-cycle visits the coarsest level
 // `shape` times in a row, multigrid.cpp:52-65) in this one launch.
@@ -556,7 +568,7 @@ unsigned plan_march(const MarchRegions &reg, int wpb, long slots, long min_rows,
 // first in every workgroup of the pass above the coarsest level and prolongs
 // from the LDS copy (write = false in all but one workgroup, which stores u
 // and the iteration statistics as the kernel does).  su: kCoarseLdsNP^2
-// doubles of LDS, lds: 16, s_norm: 1.
+// doubles of LDS, lds: 16, s_norm: unused (kept for the callers' layout).
 // (kCoarseLdsMaxN, kCoarseLdsNP: kernels.h)
 template <bool FM>
 __device__ __forceinline__ void coarse_lds_body(double *su, double *lds, double *s_norm, double *u,
@@ -564,60 +576,19 @@ __device__ __forceinline__ void coarse_lds_body(double *su, double *lds, double 
                                                 const double *v2, int n, long pitch, Coef c,
                                                 double tol, int maxit, int zero_first, int reps,
                                                 double *stats, bool write) {
+    (void)s_norm;
     constexpr int NP = kCoarseLdsNP;
-    constexpr int MR = kCoarseLdsMaxN / 16;   // residual rows per thread: 1 + ty + 16m <= 64
-    constexpr int GP = kCoarseLdsMaxN / 32;   // colour points per thread: rows 1 + r + 32p
+    constexpr int GP = kCoarseLdsMaxN / 32;   // rows per thread: 1 + gr + 32p
     const int t = threadIdx.x;
     const int tx = t & 63, ty = t >> 6;
     const int gk = t & 31, gr = t >> 5;
     const double hh = c.h * 0.5;
     // per-point constants in registers: (f, t1, t2) = FM ? (rhs/d, v1*h/2, v2*h/2)
     // : (rhs, v1, v2), exactly the operands the L2 version reads per use.
-    // Every load is issued from a clamped address before any is used (the
-    // masks are applied after): one memory round trip for the set-up, not
-    // one per point branch.
-    double gf[2][GP], gx[2][GP], gy[2][GP];   // colour points
-    int gq[2][GP];
-    bool gon[2][GP];
-    double rf[MR], rx[MR], ry[MR];            // residual points
-    int rq[MR];
-    bool ron[MR];
-#pragma unroll
-    for (int colour = 0; colour < 2; ++colour)
-#pragma unroll
-        for (int p = 0; p < GP; ++p) {
-            const int i = 1 + gr + 32 * p;
-            const int j = 1 + ((i + 1 + colour) & 1) + 2 * gk;
-            gon[colour][p] = i <= n - 1 && j <= n - 1;
-            gq[colour][p] = gon[colour][p] ? i * NP + j : NP + 1;
-            const long q = gon[colour][p] ? (long)i * pitch + j : pitch + 1;
-            gf[colour][p] = rhs[q];
-            gx[colour][p] = v1[q];
-            gy[colour][p] = v2[q];
-        }
-#pragma unroll
-    for (int m = 0; m < MR; ++m) {
-        const int i = 1 + ty + 16 * m, j = 1 + tx;
-        ron[m] = i <= n - 1 && j <= n - 1;
-        rq[m] = ron[m] ? i * NP + j : NP + 1;
-        const long q = ron[m] ? (long)i * pitch + j : pitch + 1;
-        rf[m] = rhs[q];
-        rx[m] = v1[q];
-        ry[m] = v2[q];
-    }
-    auto scale = [&](bool on, double &f, double &x, double &y) {
-        f = on ? (FM ? f * c.rdgs : f) : 0.0;
-        x = on ? (FM ? x * hh : x) : 0.0;
-        y = on ? (FM ? y * hh : y) : 0.0;
-    };
-#pragma unroll
-    for (int colour = 0; colour < 2; ++colour)
-#pragma unroll
-        for (int p = 0; p < GP; ++p)
-            scale(gon[colour][p], gf[colour][p], gx[colour][p], gy[colour][p]);
-#pragma unroll
-    for (int m = 0; m < MR; ++m) scale(ron[m], rf[m], rx[m], ry[m]);
-    {   // u into LDS: rows ty + 16m (m <= 4), columns tx, tx + 64, all loads in flight
+    // Colour c of row i sits at column 1 + ((i + 1 + c) & 1) + 2 gk: the pair
+    // (2gk + 1, 2gk + 2) holds both colours, colour 0 first on odd rows.
+    {   // u into LDS first (its loads and registers are done before the
+        // colour points' set-up): rows ty + 16m (m <= 4), columns tx, tx + 64
         constexpr int MF = (kCoarseLdsMaxN + 16) / 16;
         double a[MF][2] = {};
         if (!zero_first)   // (clamped addresses: every load in flight at once)
@@ -633,6 +604,39 @@ __device__ __forceinline__ void coarse_lds_body(double *su, double *lds, double 
                 const int i = ty + 16 * m, j = tx + 64 * h;
                 if (i <= n && j <= n) su[i * NP + j] = zero_first ? 0.0 : a[m][h];
             }
+    }
+    double gf[2][GP], gx[2][GP], gy[2][GP];
+    int gq[2][GP];
+    bool gon[2][GP];
+    const bool odd = !(gr & 1);   // row 1 + gr + 32p is odd
+    {
+        double2 lr[GP], lx[GP], ly[GP];
+#pragma unroll
+        for (int p = 0; p < GP; ++p) {   // every load in flight before any use
+            const int i = 1 + gr + 32 * p;
+            const bool ok = i <= n - 1 && 2 * gk + 2 <= n;
+            const long q = ok ? (long)i * pitch + 2 * gk + 1 : pitch + 1;
+            lr[p] = ldu2(rhs + q);
+            lx[p] = ldu2(v1 + q);
+            ly[p] = ldu2(v2 + q);
+        }
+#pragma unroll
+        for (int p = 0; p < GP; ++p) {
+            const int i = 1 + gr + 32 * p;
+#pragma unroll
+            for (int colour = 0; colour < 2; ++colour) {
+                const bool lo = (colour == 0) == odd;   // column 2gk + 1
+                const int j = lo ? 2 * gk + 1 : 2 * gk + 2;
+                const bool on = i <= n - 1 && j <= n - 1;
+                gon[colour][p] = on;
+                gq[colour][p] = on ? i * NP + j : NP + 1;
+                const double f = lo ? lr[p].x : lr[p].y, x = lo ? lx[p].x : lx[p].y,
+                             y = lo ? ly[p].x : ly[p].y;
+                gf[colour][p] = on ? (FM ? f * c.rdgs : f) : 0.0;
+                gx[colour][p] = on ? (FM ? x * hh : x) : 0.0;
+                gy[colour][p] = on ? (FM ? y * hh : y) : 0.0;
+            }
+        }
     }
     if (write && zero_first)   // (the row padding, as the L2 version leaves it)
         for (int i = ty; i <= n; i += 16)
@@ -667,26 +671,38 @@ __device__ __forceinline__ void coarse_lds_body(double *su, double *lds, double 
                 __syncthreads();
             }
             double acc = 0.0;
-            {
-                double rr[MR];
 #pragma unroll
-                for (int m = 0; m < MR; ++m) {
-                    const int q = rq[m];
-                    rr[m] = FM ? fm_res_t(rf[m], rx[m], ry[m], su[q], su[q - NP], su[q - 1],
-                                          su[q + NP], su[q + 1], c)
-                               : res_point(rf[m], rx[m], ry[m], su[q], su[q - NP], su[q - 1],
-                                           su[q + NP], su[q + 1], c);
+            for (int p = 0; p < GP; ++p) {
+                double rr[2];
+#pragma unroll
+                for (int colour = 0; colour < 2; ++colour) {
+                    const int q = gq[colour][p];
+                    const double f = gf[colour][p], x = gx[colour][p], y = gy[colour][p];
+                    rr[colour] = FM ? fm_res_t(f, x, y, su[q], su[q - NP], su[q - 1],
+                                               su[q + NP], su[q + 1], c)
+                                    : res_point(f, x, y, su[q], su[q - NP], su[q - 1],
+                                                su[q + NP], su[q + 1], c);
                 }
 #pragma unroll
-                for (int m = 0; m < MR; ++m)
-                    if (ron[m]) acc += rr[m] * rr[m];
+                for (int colour = 0; colour < 2; ++colour)
+                    if (gon[colour][p]) acc += rr[colour] * rr[colour];
+                // (one row's LDS reads at a time: the workgroup's 1024 threads
+                // leave 128 VGPRs, and all four points' reads at once spilled
+                // in the fused tile kernels)
+                __builtin_amdgcn_sched_barrier(0);
             }
-            double s = block_sum(acc, lds);
-            if (t == 0) *s_norm = sqrt(s);
+            // the block sum in every thread: wave butterfly, then the 16 wave
+            // partials in order -- the same bits everywhere, no broadcast
+            // (the next write of lds[] is behind the next iteration's two
+            // colour barriers, so no thread can overwrite what another reads)
+            acc = wave_sum(acc);
+            if ((t & 63) == 0) lds[t >> 6] = acc;
             __syncthreads();
-            res = *s_norm;
+            double s = 0.0;
+#pragma unroll
+            for (int w = 0; w < 16; ++w) s += lds[w];
+            res = sqrt(s);
             ++it;
-            __syncthreads();
         }
         total += it;
     }
