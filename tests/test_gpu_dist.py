@@ -72,6 +72,22 @@ def test_vcycles_partitioned_equal_single_N1024(G, min_rows):
     assert abs(rp - rs) <= NORM_RTOL * rs
 
 
+@pytest.mark.parametrize("min_rows", [128, 512], indirect=True)
+@pytest.mark.parametrize("G", [2, 8])
+def test_selfcheck_partitions_equal_single_N4096(G, min_rows):
+    """The partitions bench.py's RCCL self-check runs for its candidates
+    (N=4096, L=7, dist_min_rows 128 / 512; at G=8 and 512 only level 0 is
+    split, la = 1) on virtual ranks: u bitwise the one-GPU context's, fma."""
+    N, L = 4096, 7
+    dt = 1.0 / N / 10
+    fp = dict(fp_mode=_lib.FP_FMA)
+    us, ns, rs, _ = _run(N, L, dt, NU, 3, **fp)
+    up, npart, rp, info = _run(N, L, dt, NU, 3, parts=G, **fp)
+    assert info[0] == G and info[2] >= 1
+    assert np.array_equal(up, us)
+    np.testing.assert_allclose(npart, ns, rtol=NORM_RTOL)
+
+
 @pytest.mark.parametrize("G", [2, 4, 8])
 def test_vcycle_partitioned_summary_N4096(golden_summary, G):
     """Default plan (blocks >= 256 rows): reference sha256 after one V-cycle."""
