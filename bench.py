@@ -243,17 +243,20 @@ class GpuState:
                 out[k] = {"min": round(v[0], 1), "median": round(v[len(v) // 2], 1),
                           "max": round(v[-1], 1)}
         out["power_cap_W"] = self._read(f"{self.hw}/power1_cap", 1e-6) if self.hw else None
-        for f, key in (("pp_dpm_sclk", "sclk_levels"), ("pp_dpm_mclk", "mclk_levels")):
+        for f, key in (("pp_dpm_sclk", "sclk_levels"), ("pp_dpm_mclk", "mclk_levels"),
+                       ("pp_dpm_fclk", "fclk_levels"), ("pp_dpm_socclk", "socclk_levels")):
             try:
                 out[key] = open(os.path.join(self.dev, f)).read().split("\n")[:8]
                 out[key] = [x.strip() for x in out[key] if x.strip()]
             except OSError:
                 pass
-        try:
-            out["perf_level"] = open(os.path.join(self.dev,
-                                                  "power_dpm_force_performance_level")).read().strip()
-        except OSError:
-            pass
+        for f, key in (("power_dpm_force_performance_level", "perf_level"),
+                       ("current_compute_partition", "compute_partition"),
+                       ("current_memory_partition", "memory_partition")):
+            try:
+                out[key] = open(os.path.join(self.dev, f)).read().strip()
+            except OSError:
+                pass
         return out
 
 
