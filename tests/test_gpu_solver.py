@@ -142,6 +142,7 @@ def test_two_timesteps_N16384(golden_summary):
     (4096, 3, 2, 1, 0),     # config 2: 3-level V-cycle, 2 pre/post sweeps
     (512, 4, 3, 2, 0),      # W-cycle (multigrid.cpp:52)
     (512, 5, 3, 1, 1),      # correct tower
+    (1024, 5, 3, 2, 1),     # correct tower, W-cycle (fused coarsest solve, pair passes)
     (256, 7, 1, 1, 0),      # coarsest n = 4
     (2048, 2, 3, 1, 0),     # large coarsest level (host-loop coarse solve)
 ])
