@@ -101,7 +101,8 @@ def _run(world, N, L, nsmooth=3, min_rows=16, cross=False):
 
 
 @pytest.mark.parametrize("world,N,L,min_rows", [(2, 128, 4, 16), (2, 256, 5, 16),
-                                                (4, 256, 4, 16), (2, 1024, 6, 256)])
+                                                (4, 256, 4, 16), (2, 1024, 6, 256),
+                                                (2, 1024, 6, 512)])   # la = 1
 def test_partitioned_vcycle_gloo(world, N, L, min_rows):
     res = _run(world, N, L, min_rows=min_rows)
     for r in range(world):
