@@ -102,6 +102,14 @@ struct mgx_ctx {
     // rhs); step_spec = that state is ready for the next mgx_step
     bool step_next = false, step_spec = false;
     bool no_rhs_alt = false;   // the step-mode rhs did not fit in HBM: plain schedule
+    // tuning key "graph_level": the sub-cycle below a level replayed as a
+    // captured hipGraph, one per entry state (mgx.hip graph_vcycle)
+    struct Graph {
+        std::vector<long> key, end;
+        hipGraphExec_t exec = nullptr;
+    };
+    std::vector<Graph> graphs;
+    bool capturing = false;
     double step_res0 = 0;
     // profiling
     int prof = 0;   // 0 off, 1 every launch, 2 finest-level launches only

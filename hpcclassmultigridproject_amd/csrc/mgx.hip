@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -542,7 +543,96 @@ static int op_cross(mgx_ctx *c, bool store_post, bool rs = false) {
 // and visit sh+1's pre-smoothing + restriction are adjacent too, so they are
 // one cross pass as well (its u_post and norm unused): [pre | coarse | cross |
 // coarse | cross] per W-cycle instead of four level-0 passes.
+// tuning key "graph_level": > 0 = op_vcycle(c, graph_level) -- the whole
+// sub-cycle of the small levels below a level: their tile / march passes and
+// the coarsest solve -- is captured once per entry state as a hipGraph
+// (hipStreamBeginCapture on the context's own stream) and replayed, one
+// hipGraphLaunch instead of ~10 (V) or ~1000 (W) kernel launches; 0 (default)
+// = launched one by one.  The round-6 kernel trace has no idle time between
+// the launches of a cycle (profiles/r6_gaps_*.txt), so this only moves host
+// work.  Not with per-launch profiling (prof 1; prof 2 times level 0 only),
+// partitioned contexts or a borrowed stream, nor
+// where the coarsest solve loops on the host (n > kCoarseOneWgMaxN).
+long g_graph_level = 0;
+long g_tuning_epoch = 0;   // bumped by every mgx_set_tuning: graphs of older settings are stale
+long g_graph_captures = 0, g_graph_replays = 0;   // (read-only keys, for the tests)
+
+// The host state a sub-cycle from level l reads and changes: per level its
+// current u buffer, zero flag and rhs buffers, the deferred coarsest solve,
+// and the process tuning epoch.  Equal keys = the same launches on the same
+// buffers (everything else the passes read is fixed at creation / upload).
+static std::vector<long> graph_state(const mgx_ctx *c, int l) {
+    std::vector<long> k;
+    for (int i = l; i < c->L; ++i) {
+        const Level &L = c->lv[i];
+        k.push_back(L.cur);
+        k.push_back(L.zero ? 1 : 0);
+        k.push_back((long)(uintptr_t)L.rhs);
+        k.push_back((long)(uintptr_t)L.rhs_alt);
+    }
+    k.push_back(c->cf_level);
+    k.push_back(c->cf_reps);
+    k.push_back(g_tuning_epoch);
+    return k;
+}
+static void set_graph_state(mgx_ctx *c, int l, const std::vector<long> &k) {
+    size_t j = 0;
+    for (int i = l; i < c->L; ++i) {
+        Level &L = c->lv[i];
+        L.cur = (int)k[j++];
+        L.zero = k[j++] != 0;
+        L.rhs = (double *)(uintptr_t)k[j++];
+        L.rhs_alt = (double *)(uintptr_t)k[j++];
+    }
+    c->cf_level = (int)k[j++];
+    c->cf_reps = (int)k[j++];
+}
+static bool graphable(const mgx_ctx *c, int l) {
+    return g_graph_level > 0 && l == g_graph_level && !c->capturing && !c->dist &&
+           c->own_stream && c->prof != 1 && c->opt.smoother == 0 && l >= 1 && l < c->L - 1 &&
+           c->lv[c->L - 1].n <= mgx::kCoarseOneWgMaxN;
+}
+void free_graphs(mgx_ctx *c) {
+    for (auto &g : c->graphs)
+        if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    c->graphs.clear();
+}
+static int graph_vcycle(mgx_ctx *c, int l) {
+    const std::vector<long> key = graph_state(c, l);
+    for (auto &g : c->graphs)
+        if (g.key == key) {
+            HIPCHK(hipGraphLaunch(g.exec, c->stream));
+            set_graph_state(c, l, g.end);
+            ++g_graph_replays;
+            return MGX_OK;
+        }
+    if (c->graphs.size() >= 8) free_graphs(c);   // (stale entry states: start over)
+    HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    c->capturing = true;
+    const int rc = op_vcycle(c, l);
+    c->capturing = false;
+    hipGraph_t graph = nullptr;
+    const hipError_t e = hipStreamEndCapture(c->stream, &graph);
+    if (rc != MGX_OK) {
+        if (graph) (void)hipGraphDestroy(graph);
+        return rc;
+    }
+    if (e != hipSuccess) return fail(MGX_E_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+    mgx_ctx::Graph g;
+    g.key = key;
+    g.end = graph_state(c, l);
+    const hipError_t ei = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (ei != hipSuccess) return fail(MGX_E_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ei));
+    c->graphs.push_back(g);
+    ++g_graph_captures;
+    // (the capture only recorded the launches: run them now)
+    HIPCHK(hipGraphLaunch(g.exec, c->stream));
+    return MGX_OK;
+}
+
 int op_vcycle(mgx_ctx *c, int l, double *norm, bool store_post) {
+    if (!norm && graphable(c, l)) return graph_vcycle(c, l);
     if (l == 0 && norm && cross_ok(c)) {
         Level &L = c->lv[0];
         if (L.spec >= 0) {   // pre-smoothing + restriction already done
@@ -952,6 +1042,7 @@ void free_ctx(mgx_ctx *c) {
         (void)hipEventDestroy(r.e1);
     }
     for (auto e : c->pool) (void)hipEventDestroy(e);
+    free_graphs(c);
     if (c->stream && c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1592,6 +1683,12 @@ extern "C" int mgx_velocity_factored(mgx_ctx *c, int *factored) {
 // ---- tuning knobs (process-wide)
 extern "C" int mgx_set_tuning(const char *key, long value) {
     if (!key) return fail(MGX_E_ARG, "mgx_set_tuning: null key");
+    ++mgxi::g_tuning_epoch;   // captured sub-cycles of the old settings are stale
+    if (!strcmp(key, "graph_level")) {
+        if (value < 0) return fail(MGX_E_ARG, "graph_level must be >= 0");
+        mgxi::g_graph_level = value;
+        return MGX_OK;
+    }
     if (!strcmp(key, "tile_max_n")) {
         mgx::set_tile_max_n(value);
         return MGX_OK;
@@ -1715,6 +1812,14 @@ extern "C" int mgx_set_tuning(const char *key, long value) {
 }
 extern "C" int mgx_get_tuning(const char *key, long *value) {
     if (!key || !value) return fail(MGX_E_ARG, "mgx_get_tuning: null argument");
+    if (!strcmp(key, "graph_level")) {
+        *value = mgxi::g_graph_level;
+        return MGX_OK;
+    }
+    if (!strcmp(key, "graph_captures") || !strcmp(key, "graph_replays")) {
+        *value = key[6] == 'c' ? mgxi::g_graph_captures : mgxi::g_graph_replays;
+        return MGX_OK;
+    }
     if (!strcmp(key, "tile_max_n")) {
         *value = mgx::get_tile_max_n();
         return MGX_OK;

@@ -282,6 +282,37 @@ def test_wcycle_profile_counts_only_real_launches(knobs):
     assert n0 == 2 * 2, n0
 
 
+@pytest.mark.parametrize("N,L,shape,gl", [(4096, 7, 1, 3), (4096, 7, 2, 3), (2048, 6, 2, 1),
+                                          (1024, 5, 1, 2)],
+                         ids=["V4096_L3", "W4096_L3", "W2048_L1", "V1024_L2"])
+def test_graph_replay_equals_launches(N, L, shape, gl, knobs):
+    """graph_level: the sub-cycle below a level captured once per entry
+    state as a hipGraph and replayed -- u, norms, cycle counts and coarse
+    iterations bitwise the launched schedule's, through run_cycles, mg_inner
+    and time steps (W-cycles: the pair passes and the fused coarsest solve
+    with its second rhs buffer inside the graph)."""
+    out = []
+    u0, v1, v2 = init_problem(N)
+    for v in (0, gl):
+        knobs(graph_level=v)
+        c0 = _lib.get_tuning("graph_captures")
+        r0 = _lib.get_tuning("graph_replays")
+        with Multigrid(N, L, 1.0 / N / 10, NU, shape=shape, fp_mode=_lib.FP_FMA) as mg:
+            mg.upload(u0, v1, v2)
+            mg.rhs()
+            norms = [mg.run_cycles(1) for _ in range(2)] + [mg.run_cycles(3)]
+            mg.mg_inner()
+            cyc = [mg.step(1e-6) for _ in range(2)]
+            out.append((mg.download(), norms, cyc, mg.coarse_iterations(),
+                        _lib.get_tuning("graph_captures") - c0,
+                        _lib.get_tuning("graph_replays") - r0))
+    (ua, na, ca, ia, cap_a, rep_a), (ub, nb, cb, ib, cap_b, rep_b) = out
+    assert np.array_equal(ua, ub)
+    assert na == nb and ca == cb and ia == ib
+    assert cap_a == 0 and rep_a == 0
+    assert cap_b >= 1 and rep_b >= 1, (cap_b, rep_b)   # the graph path really ran
+
+
 def test_negative_diagonal_routes_to_general_division(cross, oracle_mod):
     """nu > 0 large enough that the finest level's diagonal 1-4*rr*nu is
     negative: the unguarded cross kernel's division form assumes d > 0, so the
